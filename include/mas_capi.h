@@ -1,0 +1,145 @@
+/*
+ * mas_capi.h -- C ABI of the MI355X-native multilevel additive Schwarz (MAS)
+ * preconditioner.  Plain pointers and sizes only; no HIP or torch types.
+ *
+ * Drop-in boundary.  Each entry point replaces one member of the reference
+ * plugin surface (V-Sekai/preconditioner-for-cloth-and-deformable-body-simulation,
+ * SeSchwarzPreconditioner.h, namespace SE):
+ *
+ *   mas_allocate      <- SeSchwarzPreconditioner::AllocatePrecoditioner
+ *                        (SeSchwarzPreconditioner.h:56, .cpp:38-65) together
+ *                        with the public inputs m_positions / m_edges /
+ *                        m_faces / m_neighbours (SeSchwarzPreconditioner.h:44-51)
+ *   mas_prepare       <- SeSchwarzPreconditioner::PreparePreconditioner
+ *                        (SeSchwarzPreconditioner.h:59-60, .cpp:67-98)
+ *   mas_apply         <- SeSchwarzPreconditioner::Preconditioning
+ *                        (SeSchwarzPreconditioner.h:63, .cpp:100-110)
+ *   mas_apply_device  <- same, on device-resident vectors (the benchmarked path)
+ *
+ * Memory layouts are the reference's:
+ *   vectors  float[4] per vertex (SeVec3fSimd, 16 B, w ignored on input,
+ *            written 0 on output)                   SeVectorSimd.h:45-57
+ *   3x3      float[9] column-major (SeMatrix3f)     SeMatrix.h:650-682
+ *   Int4     int[4]                                 SeVector.h:395
+ *   contact  48-byte EfSet / EeSet / VfSet records  SeCollisionElements.h:33-58
+ *   counts   unsigned[], only the total at [nE] / [nE] / [nV] is read
+ *                                                   .cpp:306-308
+ *
+ * All functions return MAS_OK (0) or a negative mas_status.  A handle is not
+ * thread-safe (neither is the reference object).  Host-pointer functions
+ * synchronise the handle's stream before returning; *_device functions are
+ * asynchronous on the given stream (NULL = the handle's own stream).
+ */
+#ifndef MAS_CAPI_H
+#define MAS_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAS_ABI_VERSION 1
+
+typedef enum {
+    MAS_OK = 0,
+    MAS_ERR_ARG = -1,      /* null / out-of-range argument                       */
+    MAS_ERR_HIP = -2,      /* HIP runtime failure (see mas_last_error)           */
+    MAS_ERR_CAPACITY = -3, /* a size limit was exceeded (stencils, levels, ...)  */
+    MAS_ERR_STATE = -4,    /* call order violated (prepare before allocate, ...)  */
+    MAS_ERR_LEVELS = -5,   /* more than 5 levels requested (reference B-6)        */
+    MAS_ERR_NOMEM = -6,    /* device allocation failed                           */
+    MAS_ERR_NO_DEVICE = -7 /* no HIP device / kernels not loadable                */
+} mas_status;
+
+typedef struct mas_context* mas_handle;
+
+typedef struct {
+    int max_levels;    /* 0 = reference rule (ComputeLevelNums .cpp:112-135), else min(natural, max_levels) */
+    int resort_period; /* 0 = reference behaviour (sort on first Allocate only, B-1); k>0: re-sort every k calls */
+    int fix_vf_bary;   /* 0 = parity with reference release build (B-2); 1 = -(1-b0-b1) */
+    int device;        /* HIP device ordinal; -1 = current device */
+    int reserved[12];
+} mas_config;
+
+typedef struct {
+    int num_verts, num_edges, num_faces;
+    int num_levels;          /* levels in use */
+    int natural_levels;      /* reference ComputeLevelNums */
+    int total_clusters;      /* levelSize[L].y: node ids [0, total_clusters) */
+    int num_blocks;          /* total_clusters / 32 */
+    int num_fine_blocks;     /* ceil(nV / 32) */
+    int max_neighbors;       /* max valence + 1 */
+    int num_stencils;
+    int level_size[2 * 9];   /* (count, begin) for levels 0..num_levels */
+    int64_t inv_bytes;       /* bytes of packed inverses on device */
+    int64_t device_bytes;    /* total device memory held by the handle */
+} mas_info;
+
+typedef struct {
+    /* milliseconds of the most recent call of each phase (device time) */
+    double allocate_ms, prepare_ms, apply_ms;
+    double prepare_levels_ms, prepare_assemble_ms, prepare_factor_ms;
+    /* per-kernel device time of the most recent mas_apply_device with
+     * profiling enabled (mas_set_profiling), milliseconds */
+    double apply_restrict_ms, apply_coarse_ms, apply_fine_ms;
+    int64_t apply_calls;
+} mas_stats;
+
+/* lifecycle */
+int mas_version(void);
+int mas_create(mas_handle* out, const mas_config* cfg /* may be NULL */);
+int mas_destroy(mas_handle h);
+const char* mas_last_error(mas_handle h);
+
+/* AllocatePrecoditioner + the public input members.
+ * pos4[nV][4]; CSR nbr_starts[nV+1], nbr_idx[nbr_starts[nV]] (symmetric, no self);
+ * edges4[nE][4], faces4[nF][4] (may be NULL when no EF/EE/VF contacts are used).
+ * Host pointers; copied. */
+int mas_allocate(mas_handle h, int nV, int nE, int nF, const float* pos4, const int* nbr_starts,
+                 const int* nbr_idx, const int* edges4, const int* faces4);
+
+/* PreparePreconditioner with host pointers (copied to the device).
+ * diag9[nV][9], off9[nnz][9], ranges[nV+1] (== nbr_starts).  ef/ee/vf may be
+ * NULL when their count array is NULL or holds 0. */
+int mas_prepare(mas_handle h, const float* diag9, const float* off9, const int* ranges, const void* ef,
+                const void* ee, const void* vf, const unsigned* ef_counts, const unsigned* ee_counts,
+                const unsigned* vf_counts);
+
+/* PreparePreconditioner with device pointers.  Contact records stay host
+ * pointers (they are small and their totals drive the launch sizes). */
+int mas_prepare_device(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges,
+                       const void* ef, const void* ee, const void* vf, const unsigned* ef_counts,
+                       const unsigned* ee_counts, const unsigned* vf_counts, void* stream);
+
+/* Preconditioning(z, r, dim): host vectors [nV][4]. */
+int mas_apply(mas_handle h, float* z4, const float* r4);
+
+/* Preconditioning on device vectors d_z4, d_r4 ([nV][4], 16-B aligned).
+ * stream: hipStream_t (NULL = handle stream).  Asynchronous. */
+int mas_apply_device(mas_handle h, float* d_z4, const float* d_r4, void* stream);
+
+/* Record per-kernel HIP events inside mas_apply_device (for mas_stats). */
+int mas_set_profiling(mas_handle h, int enable);
+
+/* introspection / parity */
+int mas_get_info(mas_handle h, mas_info* out);
+int mas_get_stats(mas_handle h, mas_stats* out);
+/* Level maps, host outputs; any pointer may be NULL.
+ * morton[nV] (by original id), s2o[nV], o2s[nV],
+ * coarse_space_tables[L*nV], going_next[total_clusters], coarse_tables[nV*4],
+ * fine_connect_mask[nV]. */
+int mas_get_maps(mas_handle h, uint64_t* morton, int* s2o, int* o2s, int* coarse_space_tables,
+                 int* going_next, int* coarse_tables, unsigned* fine_connect_mask);
+/* ELL neighbour table [max_neighbors][nV] and counts [nV] (MapHessianTable). */
+int mas_get_neighbors(mas_handle h, int* nbr_num, int* nbr);
+/* Dense assembled block (96x96 row-major, zero-diagonal -> identity applied)
+ * and its inverse unpacked to 96x96. */
+int mas_get_block_matrix(mas_handle h, int blk, float* out96x96);
+int mas_get_block_inverse(mas_handle h, int blk, float* out96x96);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAS_CAPI_H */

@@ -1,0 +1,383 @@
+// k_assemble.hip -- dense 96x96 subdomain blocks from the CSR Hessian and the
+// contact stencils (PrepareCollisionHessian .cpp:1164-1227, PrepareHessian
+// .cpp:1229-1345).
+//
+// Layout: block b is a row-major 96x96 fp32 matrix at dense + 9216 b; the 3x3
+// entry (row node x, column node y) of block b holds what the reference keeps
+// in m_hessian32[y][32 b + x] (.cpp:1363-1375).
+//
+// Why the summation order is reproduced exactly: inside a cluster the spring
+// terms of the diagonal and off-diagonal blocks cancel (K - K), so a coarse
+// entry is a small difference of large fp32 sums, and coarse blocks are badly
+// conditioned (~1e5).  A different association moves z by ~1e-4 relative.
+// Every sum below is therefore a strict left fold in the reference's
+// single-thread order (vertex order, then ELL neighbour order; hash-map pushes
+// in node-id order, see oracle/mas_oracle.c), computed in parallel over
+// independent targets:
+//   k_level0      per vertex: block-0 diagonal and same-bank entries (single
+//                 writer), od(u) = diag + additional + level-0 entries
+//                 (oldDiagonal, .cpp:1270-1298), count of coarse edges
+//   k_records     coarse edges (u, k) with first common-bank level 1..L-1, in
+//                 (u, k) order
+//   k_fold_entries  one thread per coarse entry (row, col), records sorted
+//                 stably by (row, col): entry += mat in (u, k) order
+//   k_diag1       one thread per level-0 bank: diag(anc1(u)) += od(u) (.cpp:1309-1312)
+//   k_table       one thread per level-l node (l >= 2): the diagTable fold
+//                 (.cpp:1299-1343): over member vertices in order, level-(l-1)
+//                 edge mats and (l = 2) od(u); then the children's tables in
+//                 id order; diag += table.
+// Contact stencils (only present in the contact configuration) still
+// accumulate with fp32 atomics, as the reference does at CPU_THREAD_NUM > 1.
+#include <hipcub/hipcub.hpp>
+
+#include "mas_internal.h"
+
+namespace mas {
+
+struct EdgeRec {
+    int lam;  // first common-bank level, 1..L-1
+    int row;  // anc_lam(u) (global node id)
+    int col;  // anc_lam(v)
+    int mat;  // index into off9
+};
+
+__device__ __forceinline__ float* entry(float* dense, unsigned rowNode, unsigned colNode) {
+    return dense + (size_t)(rowNode >> 5) * kDenseFloats + (3 * (rowNode & 31)) * 96 + 3 * (colNode & 31);
+}
+
+__device__ __forceinline__ int climb(const int* __restrict__ gn, int L, unsigned& my, unsigned& ot) {
+    int level = 0;
+    while ((my >> 5) != (ot >> 5) && level < L) {
+        level++;
+        my = (unsigned)gn[my];
+        ot = (unsigned)gn[ot];
+    }
+    return level;
+}
+
+// 3x3 stored column-major in the inputs; entries of the dense block are row-major.
+__device__ __forceinline__ void add_colmajor(float* e, const float* __restrict__ m) {
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], m[c * 3 + r]);
+}
+
+// ---------------------------------------------------------------------------
+// contacts (reference semantics, fp32 atomics)
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_collision_hessian(const DevStencil* __restrict__ st, int n,
+                                                           const int* __restrict__ gn, int L,
+                                                           float* __restrict__ dense, float* __restrict__ additional) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    DevStencil s = st[i];
+    float ds[3] = {__fmul_rn(s.dir[0], s.stiff), __fmul_rn(s.dir[1], s.stiff), __fmul_rn(s.dir[2], s.stiff)};
+    float hm[3][3];  // OuterProduct(d, d * stiff), SeMatrix.h:352-363
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) hm[r][c] = __fmul_rn(s.dir[r], ds[c]);
+    for (int it = 0; it < s.n; ++it) {  // .cpp:1214-1217: additional[idx] += h * w^2
+        const float w2 = __fmul_rn(s.w[it], s.w[it]);
+        float* a = additional + 9 * (size_t)s.idx[it];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) atomicAdd(a + r * 3 + c, __fmul_rn(hm[r][c], w2));
+    }
+    for (int a = 0; a < s.n; ++a)  // AdditionalSchwarzHessian2, .cpp:1164-1199
+        for (int b = a + 1; b < s.n; ++b) {
+            const float ww = __fmul_rn(s.w[a], s.w[b]);
+            unsigned my = (unsigned)s.idx[a], ot = (unsigned)s.idx[b];
+            const int level = climb(gn, L, my, ot);
+            if (level >= L) continue;
+            float* e0 = entry(dense, my, ot);
+            float* e1 = entry(dense, ot, my);
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) {
+                    const float t = __fmul_rn(ww, hm[r][c]);
+                    atomicAdd(e0 + r * 96 + c, t);
+                    atomicAdd(e1 + r * 96 + c, t);
+                }
+            if (level < L - 1) {
+                const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) {
+                        const float t = __fmul_rn(ww, hm[r][c]);
+                        if (pm == po) {
+                            atomicAdd(additional + 9 * (size_t)pm + r * 3 + c, __fmul_rn(t, 2.0f));
+                        } else {
+                            atomicAdd(additional + 9 * (size_t)pm + r * 3 + c, t);
+                            atomicAdd(additional + 9 * (size_t)po + r * 3 + c, t);
+                        }
+                    }
+            }
+        }
+}
+
+// .cpp:1236-1252: coarse additional -> own diagonal and every ancestor.
+__global__ __launch_bounds__(256) void k_coarse_additional(int begin1, int tc, const int* __restrict__ gn,
+                                                           const float* __restrict__ additional,
+                                                           float* __restrict__ dense) {
+    const int vid = begin1 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (vid >= tc) return;
+    const float* a = additional + 9 * (size_t)vid;
+    bool any = false;
+    for (int e = 0; e < 9; ++e) any |= a[e] != 0.f;
+    if (!any) return;
+    int my = vid;
+    while (my < tc) {
+        float* d = entry(dense, my, my);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) atomicAdd(d + r * 96 + c, a[r * 3 + c]);
+        my = gn[my];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CSR Hessian (deterministic, reference order)
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_level0(int nV, int L, const int* __restrict__ s2o,
+                                                const int* __restrict__ nbrNum, const int* __restrict__ nbr,
+                                                const int* __restrict__ gn, const float* __restrict__ diag9,
+                                                const float* __restrict__ off9, const int* __restrict__ ranges,
+                                                const float* __restrict__ additional, float* __restrict__ dense,
+                                                float* __restrict__ od, int* __restrict__ recCnt) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nV) return;
+    const int o = s2o[v];
+    float acc[9];
+    const float* d = diag9 + 9 * (size_t)o;
+    const float* ad = additional + 9 * (size_t)v;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);  // .cpp:1270
+    {
+        float* e = entry(dense, v, v);  // .cpp:1271
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], acc[r * 3 + c]);
+    }
+    const int num = nbrNum[v];
+    const size_t base = (size_t)ranges[o];
+    int cnt = 0;
+    for (int k = 1; k < num; ++k) {
+        unsigned my = (unsigned)v, ot = (unsigned)nbr[(size_t)k * nV + v];
+        const int level = climb(gn, L, my, ot);
+        if (level >= L) continue;
+        if (level == 0) {
+            const float* m = off9 + 9 * (base + k - 1);
+            add_colmajor(entry(dense, my, ot), m);
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[c * 3 + r]);
+        } else {
+            cnt++;
+        }
+    }
+    for (int e = 0; e < 9; ++e) od[9 * (size_t)v + e] = acc[e];
+    recCnt[v] = cnt;
+}
+
+__global__ __launch_bounds__(256) void k_records(int nV, int L, const int* __restrict__ s2o,
+                                                 const int* __restrict__ nbrNum, const int* __restrict__ nbr,
+                                                 const int* __restrict__ gn, const int* __restrict__ ranges,
+                                                 const int* __restrict__ recOff, EdgeRec* __restrict__ rec,
+                                                 unsigned long long* __restrict__ keys, int* __restrict__ ids) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nV) return;
+    const int o = s2o[v];
+    const int num = nbrNum[v];
+    const int base = ranges[o];
+    int w = recOff[v];
+    for (int k = 1; k < num; ++k) {
+        unsigned my = (unsigned)v, ot = (unsigned)nbr[(size_t)k * nV + v];
+        const int level = climb(gn, L, my, ot);
+        if (level == 0 || level >= L) continue;
+        rec[w] = EdgeRec{level, (int)my, (int)ot, base + k - 1};
+        keys[w] = ((unsigned long long)my << 32) | ot;
+        ids[w] = w;
+        ++w;
+    }
+}
+
+// one thread per run of equal (row, col) in the stably sorted record keys
+__global__ __launch_bounds__(256) void k_fold_entries(int n, const unsigned long long* __restrict__ keys,
+                                                      const int* __restrict__ ids, const EdgeRec* __restrict__ rec,
+                                                      const float* __restrict__ off9, float* __restrict__ dense) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long key = keys[i];
+    if (i > 0 && keys[i - 1] == key) return;
+    const EdgeRec r0 = rec[ids[i]];
+    float* e = entry(dense, (unsigned)r0.row, (unsigned)r0.col);
+    float acc[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
+    for (int j = i; j < n && keys[j] == key; ++j) {
+        const float* m = off9 + 9 * (size_t)rec[ids[j]].mat;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[c * 3 + r]);
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
+}
+
+// level-1 diagonal: one thread per level-0 bank, members in lane order
+__global__ __launch_bounds__(256) void k_diag1(int nV, const int* __restrict__ gn, const float* __restrict__ od,
+                                               float* __restrict__ dense) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w * 32 >= nV) return;
+    for (int u = w * 32; u < w * 32 + 32 && u < nV; ++u) {
+        const unsigned p = (unsigned)gn[u];
+        float* e = entry(dense, p, p);
+        const float* a = od + 9 * (size_t)u;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], a[r * 3 + c]);
+    }
+}
+
+// Stable grouping boundaries: off[key] = first sorted position of key.
+__global__ __launch_bounds__(256) void k_bounds(int n, const int* __restrict__ sortedKeys, int nKeys,
+                                                int* __restrict__ off) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int k = sortedKeys[i];
+    if (i == 0 || sortedKeys[i - 1] != k) off[k] = i;
+    if (i == n - 1) off[nKeys] = n;
+}
+
+// diagTable fold for level l >= 2, one thread per level-l node P.
+__global__ __launch_bounds__(256) void k_table(int l, int L, int count, int begin, int beginPrev,
+                                               const int* __restrict__ vlist, const int* __restrict__ voff,
+                                               const int* __restrict__ cstPrev2, const int* __restrict__ gn,
+                                               const int* __restrict__ recOff, const EdgeRec* __restrict__ rec,
+                                               const float* __restrict__ off9, const float* __restrict__ od,
+                                               float* __restrict__ tab, float* __restrict__ dense) {
+    const int local = blockIdx.x * blockDim.x + threadIdx.x;
+    if (local >= count) return;
+    const int P = begin + local;
+    float t[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    bool present = false;
+    const int b = voff[local], e = voff[local + 1];
+    for (int i = b; i < e; ++i) {
+        const int u = vlist[i];
+        for (int j = recOff[u]; j < recOff[u + 1]; ++j) {
+            const EdgeRec r = rec[j];
+            if (r.lam != l - 1) continue;
+            const float* m = off9 + 9 * (size_t)r.mat;
+            for (int rr = 0; rr < 3; ++rr)
+                for (int c = 0; c < 3; ++c) t[rr * 3 + c] = __fadd_rn(t[rr * 3 + c], m[c * 3 + rr]);
+            present = true;
+        }
+        if (l == 2) {
+            const float* a = od + 9 * (size_t)u;
+            for (int q = 0; q < 9; ++q) t[q] = __fadd_rn(t[q], a[q]);
+            present = true;
+        }
+    }
+    if (l >= 3) {  // pushes of the level-(l-1) tables, children in id order (.cpp:1333-1341)
+        const int u0 = vlist[b];
+        const int childLocal = cstPrev2[u0];  // level-(l-1) local id of the first member
+        const int bankBase = beginPrev + (childLocal & ~31);
+        for (int j = 0; j < 32; ++j) {
+            const int c = bankBase + j;
+            if (gn[c] != P) continue;
+            const float* a = tab + 9 * (size_t)c;
+            for (int q = 0; q < 9; ++q) t[q] = __fadd_rn(t[q], a[q]);
+            present = true;
+        }
+    }
+    for (int q = 0; q < 9; ++q) tab[9 * (size_t)P + q] = t[q];
+    if (present) {
+        float* d = entry(dense, (unsigned)P, (unsigned)P);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) d[r * 96 + c] = __fadd_rn(d[r * 96 + c], t[r * 3 + c]);
+    }
+}
+
+int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s) {
+    const int nV = h->nV, L = h->L, tc = h->totalClusters;
+    int rc;
+    const size_t denseBytes = (size_t)h->nBlk * kDenseFloats * 4;
+    if ((rc = ensure(h, h->dense, denseBytes)) || (rc = ensure(h, h->additional, (size_t)(tc + 1) * 36)) ||
+        (rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
+        (rc = ensure(h, h->recOff, (size_t)(nV + 1) * 4)) || (rc = ensure(h, h->tab, (size_t)(tc + 1) * 36)))
+        return rc;
+    if ((rc = hip_check(h, hipMemsetAsync(h->dense.p, 0, denseBytes, s), "memset dense")) ||
+        (rc = hip_check(h, hipMemsetAsync(h->additional.p, 0, (size_t)(tc + 1) * 36, s), "memset additional")) ||
+        (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt")))
+        return rc;
+    float* dense = P<float>(h->dense);
+    float* add = P<float>(h->additional);
+    const int* gn = P<int>(h->goingNext);
+    const int begin1 = h->levelSize[3];
+    if (h->nStencil) {
+        k_collision_hessian<<<cdiv(h->nStencil, 256), 256, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil, gn, L,
+                                                                   dense, add);
+        if (tc > begin1) k_coarse_additional<<<cdiv(tc - begin1, 256), 256, 0, s>>>(begin1, tc, gn, add, dense);
+    }
+    k_level0<<<cdiv(nV, 256), 256, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), gn, d_diag9,
+                                           d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt));
+    if (L == 1) return hip_check(h, hipGetLastError(), "assembly kernels");
+
+    // coarse edge records in (u, k) order
+    size_t tmp = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, P<int>(h->recCnt), P<int>(h->recOff), nV + 1, s);
+    if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
+    if ((rc = hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, P<int>(h->recCnt), P<int>(h->recOff),
+                                                            nV + 1, s),
+                        "record scan")))
+        return rc;
+    int nRec = 0;
+    if ((rc = hip_check(h, hipMemcpyAsync(&nRec, P<int>(h->recOff) + nV, 4, hipMemcpyDeviceToHost, s), "D2H nRec")) ||
+        (rc = hip_check(h, hipStreamSynchronize(s), "nRec sync")))
+        return rc;
+    const size_t nr = nRec > 0 ? nRec : 1;
+    if ((rc = ensure(h, h->rec, nr * sizeof(EdgeRec))) || (rc = ensure(h, h->recKeys, nr * 8)) ||
+        (rc = ensure(h, h->recKeysSorted, nr * 8)) || (rc = ensure(h, h->recIds, nr * 4)) ||
+        (rc = ensure(h, h->recIdsSorted, nr * 4)))
+        return rc;
+    EdgeRec* rec = P<EdgeRec>(h->rec);
+    k_records<<<cdiv(nV, 256), 256, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), gn, d_ranges,
+                                            P<int>(h->recOff), rec, P<unsigned long long>(h->recKeys),
+                                            P<int>(h->recIds));
+    if (nRec > 0) {
+        tmp = 0;
+        hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, P<unsigned long long>(h->recKeys),
+                                           P<unsigned long long>(h->recKeysSorted), P<int>(h->recIds),
+                                           P<int>(h->recIdsSorted), nRec, 0, 64, s);
+        if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
+        if ((rc = hip_check(h,
+                            hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, P<unsigned long long>(h->recKeys),
+                                                               P<unsigned long long>(h->recKeysSorted),
+                                                               P<int>(h->recIds), P<int>(h->recIdsSorted), nRec, 0,
+                                                               64, s),
+                            "record sort")))
+            return rc;
+        k_fold_entries<<<cdiv(nRec, 256), 256, 0, s>>>(nRec, P<unsigned long long>(h->recKeysSorted),
+                                                       P<int>(h->recIdsSorted), rec, d_off9, dense);
+    }
+    k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
+
+    // diagTable folds, levels 2..L-1
+    if ((rc = ensure(h, h->vkeys, (size_t)nV * 4)) || (rc = ensure(h, h->vlist, (size_t)nV * 4)) ||
+        (rc = ensure(h, h->voff, (size_t)(nV + 1) * 4)))
+        return rc;
+    for (int l = 2; l < L; ++l) {
+        const int count = h->levelSize[2 * l], begin = h->levelSize[2 * l + 1];
+        const int beginPrev = h->levelSize[2 * (l - 1) + 1];
+        const int* cstPrev = P<int>(h->cst) + (size_t)(l - 1) * nV;  // level-l local id per vertex
+        const int* cstPrev2 = P<int>(h->cst) + (size_t)(l - 2) * nV; // level-(l-1) local id per vertex
+        tmp = 0;
+        hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, cstPrev, P<int>(h->vkeys), P<int>(h->iota), P<int>(h->vlist),
+                                           nV, 0, 32, s);
+        if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
+        if ((rc = hip_check(h,
+                            hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, cstPrev, P<int>(h->vkeys),
+                                                               P<int>(h->iota), P<int>(h->vlist), nV, 0, 32, s),
+                            "vertex-list sort")))
+            return rc;
+        k_bounds<<<cdiv(nV, 256), 256, 0, s>>>(nV, P<int>(h->vkeys), count, P<int>(h->voff));
+        k_table<<<cdiv(count, 256), 256, 0, s>>>(l, L, count, begin, beginPrev, P<int>(h->vlist), P<int>(h->voff),
+                                                 cstPrev2, gn, P<int>(h->recOff), rec, d_off9, P<float>(h->od),
+                                                 P<float>(h->tab), dense);
+    }
+    return hip_check(h, hipGetLastError(), "assembly kernels");
+}
+
+}  // namespace mas

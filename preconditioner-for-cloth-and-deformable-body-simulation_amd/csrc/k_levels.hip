@@ -1,0 +1,358 @@
+// k_levels.hip -- contact stencils and the aggregation hierarchy on the GPU
+// (PrepareCollisionStencils .cpp:304-413, ReorderRealtime .cpp:415-1162).
+//
+// The reference emulates 32-lane warps on the CPU; here one 32-lane group of
+// a wave64 is one "bank" (two banks per wave).  Bank-local state (connection
+// masks for the bit-BFS) lives in LDS; cross-bank ids come from a device-wide
+// exclusive scan (hipcub) -- the reference's block-prefix loop has a bug above
+// 33 792 nodes per level (B-5), the scan is correct and identical below it.
+// Everything here is integer work and is bit-exact with the reference.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "mas_internal.h"
+
+namespace mas {
+
+// ---------------------------------------------------------------------------
+// contact stencils
+// ---------------------------------------------------------------------------
+
+// flag[i]: 1 = valid record, 0 = skipped (negative id, .cpp:330,359,385),
+// 2 = id out of range (reference UB; reported as MAS_ERR_ARG).
+__global__ __launch_bounds__(256) void k_stencil_flags(const unsigned char* __restrict__ raw, int efNum, int eeNum,
+                                                       int total, int nV, int nE, int nF, int* __restrict__ flag) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int* rec = reinterpret_cast<const int*>(raw + 48 * (size_t)i);
+    int a = rec[0], b = rec[1];
+    int f = 1;
+    if (a < 0 || b < 0) f = 0;
+    else if (i < efNum) f = (a < nE && b < nF) ? 1 : 2;
+    else if (i < efNum + eeNum) f = (a < nE && b < nE) ? 1 : 2;
+    else f = (a < nV && b < nF) ? 1 : 2;
+    flag[i] = f;
+}
+
+__global__ __launch_bounds__(256) void k_stencil_build(const unsigned char* __restrict__ raw, int efNum, int eeNum,
+                                                       int total, const int* __restrict__ flag,
+                                                       const int* __restrict__ slot, const int4* __restrict__ edges,
+                                                       const int4* __restrict__ faces, const int* __restrict__ o2s,
+                                                       int fixVfBary, DevStencil* __restrict__ out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total || flag[i] != 1) return;
+    const unsigned char* p = raw + 48 * (size_t)i;
+    const int* pi = reinterpret_cast<const int*>(p);
+    const float* pf = reinterpret_cast<const float*>(p);
+    DevStencil s;
+    int vidx[5] = {0, 0, 0, 0, 0};
+    s.stiff = pf[2];
+    s.dir[0] = pf[8];
+    s.dir[1] = pf[9];
+    s.dir[2] = pf[10];
+    if (i < efNum) {  // EfSet: bary Float3 @12; .cpp:326-354
+        int4 e = edges[pi[0]], f = faces[pi[1]];
+        float b0 = pf[3], b1 = pf[4], b2 = pf[5];
+        s.n = 5;
+        s.nFirst = 2;
+        vidx[0] = e.x; vidx[1] = e.y; vidx[2] = f.x; vidx[3] = f.y; vidx[4] = f.z;
+        s.w[0] = b0;
+        s.w[1] = __fsub_rn(1.f, b0);
+        s.w[2] = -b1;
+        s.w[3] = -b2;
+        s.w[4] = -__fsub_rn(__fsub_rn(1.f, b1), b2);
+    } else if (i < efNum + eeNum) {  // EeSet: bary Float2 @16; .cpp:355-380 (B-3 fixed)
+        int4 e0 = edges[pi[0]], e1 = edges[pi[1]];
+        float b0 = pf[4], b1 = pf[5];
+        s.n = 4;
+        s.nFirst = 2;
+        vidx[0] = e0.x; vidx[1] = e0.y; vidx[2] = e1.x; vidx[3] = e1.y;
+        s.w[0] = b0;
+        s.w[1] = __fsub_rn(1.f, b0);
+        s.w[2] = -b1;
+        s.w[3] = -__fsub_rn(1.f, b1);
+        s.w[4] = 0.f;
+    } else {  // VfSet: bary Float2 @16, B-2 reads the float @24; .cpp:381-405
+        int4 f = faces[pi[1]];
+        float b0 = pf[4], b1 = pf[5], b2 = pf[6];
+        s.n = 4;
+        s.nFirst = 3;
+        vidx[0] = f.x; vidx[1] = f.y; vidx[2] = f.z; vidx[3] = pi[0];
+        s.w[0] = -b0;
+        s.w[1] = -b1;
+        s.w[2] = fixVfBary ? -__fsub_rn(__fsub_rn(1.f, b0), b1) : -__fsub_rn(1.f, b2);
+        s.w[3] = 1.f;
+        s.w[4] = 0.f;
+    }
+    for (int k = 0; k < 5; ++k) s.idx[k] = (k < s.n) ? o2s[vidx[k]] : 0;  // MapCollisionStencilIndices
+    out[slot[i]] = s;
+}
+
+// BuildCollisionConnection, .cpp:514-563 (pCoarse == nullptr at level 0)
+__global__ __launch_bounds__(256) void k_collision_connect(const DevStencil* __restrict__ st, int n,
+                                                           const int* __restrict__ pCoarse,
+                                                           unsigned* __restrict__ connect) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    DevStencil s = st[i];
+    int idx[5];
+    unsigned msk[5] = {0, 0, 0, 0, 0};
+    for (int k = 0; k < 5; ++k) idx[k] = (k < s.n) ? (pCoarse ? pCoarse[s.idx[k]] : s.idx[k]) : 0;
+    for (int a = 0; a < s.n; ++a)
+        for (int b = a + 1; b < s.n; ++b) {
+            unsigned my = (unsigned)idx[a], ot = (unsigned)idx[b];
+            if (my == ot) continue;
+            if ((my >> 5) == (ot >> 5) && a < s.nFirst && b >= s.nFirst) {
+                msk[a] |= 1u << (ot & 31);
+                msk[b] |= 1u << (my & 31);
+            }
+        }
+    for (int k = 0; k < s.n; ++k)
+        if (msk[k]) atomicOr(&connect[idx[k]], msk[k]);
+}
+
+// ---------------------------------------------------------------------------
+// aggregation hierarchy
+// ---------------------------------------------------------------------------
+
+// BuildConnectMaskL0, .cpp:447-511: same-bank neighbour bits, compact the rest.
+__global__ __launch_bounds__(256) void k_connect_l0(int nV, int* __restrict__ numRem, int* __restrict__ rem,
+                                                    unsigned* __restrict__ fineMask) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nV) return;
+    int warp = v >> 5, num = numRem[v], nk = 0;
+    unsigned msk = 1u << (v & 31);
+    for (int k = 0; k < num; ++k) {
+        int u = rem[(size_t)k * nV + v];
+        if ((u >> 5) == warp) msk |= 1u << (u & 31);
+        else rem[(size_t)(nk++) * nV + v] = u;
+    }
+    numRem[v] = nk;
+    fineMask[v] = msk;
+}
+
+// BuildConnectMaskLx, .cpp:743-871.  Every member of a level-0 component maps
+// to the same level-l node, so OR-ing each vertex's same-bank bits straight
+// into nextMask[coarse] is the reference's per-component OR (see oracle).
+__global__ __launch_bounds__(256) void k_connect_lx(int nV, const int* __restrict__ cstPrev, int* __restrict__ numRem,
+                                                    int* __restrict__ rem, unsigned* __restrict__ nextMask) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nV) return;
+    unsigned cv = (unsigned)cstPrev[v], msk = 0;
+    int kn = numRem[v], nk = 0;
+    for (int k = 0; k < kn; ++k) {
+        int u = rem[(size_t)k * nV + v];
+        unsigned cu = (unsigned)cstPrev[u];
+        if ((cv >> 5) == (cu >> 5)) msk |= 1u << (cu & 31);
+        else rem[(size_t)(nk++) * nV + v] = u;
+    }
+    numRem[v] = nk;
+    if (msk) atomicOr(&nextMask[cv], msk);
+}
+
+// PreparePrefixSumL0 (.cpp:565-628) / NextLevelCluster (.cpp:873-961):
+// per-bank bit-BFS closure from each lane, leader = lowest lane of its mask,
+// leaders counted per bank.
+__global__ __launch_bounds__(256) void k_bank_closure(int n, unsigned* __restrict__ masks, int* __restrict__ counts) {
+    __shared__ unsigned cache[256];
+    const int t = threadIdx.x, lane = t & 31, gbase = t & ~31;
+    const int c = blockIdx.x * 256 + t;
+    cache[t] = (1u << lane) | (c < n ? masks[c] : 0u);
+    __syncthreads();
+    bool leader = false;
+    if (c < n) {
+        unsigned m = cache[t], visited = 1u << lane;
+        while (m != 0xFFFFFFFFu) {
+            unsigned todo = visited ^ m;
+            if (!todo) break;
+            unsigned nxt = (unsigned)__ffs(todo) - 1u;
+            visited |= 1u << nxt;
+            m |= cache[gbase + nxt];
+        }
+        masks[c] = m;
+        leader = __popc(m & ((1u << lane) - 1u)) == 0;
+    }
+    unsigned long long b = __ballot(leader);
+    if (lane == 0 && (c & ~31) < n) counts[c >> 5] = __popc((unsigned)(b >> (t & 32)));
+}
+
+// BuildLevel1 (.cpp:630-740) / PrefixSumLx (.cpp:963-1072): cluster id =
+// bank prefix + rank of the lowest lane of the component among the leaders.
+__global__ __launch_bounds__(256) void k_assign_ids(int n, int level, int begin, int nv32,
+                                                    unsigned* __restrict__ masks, const int* __restrict__ prefix,
+                                                    const int* __restrict__ counts, int nBanks,
+                                                    int* __restrict__ cst0, int* __restrict__ goingNext,
+                                                    int* __restrict__ levelTotal) {
+    const int t = threadIdx.x, lane = t & 31;
+    const int c = blockIdx.x * 256 + t;
+    unsigned m = c < n ? masks[c] : 0u;
+    bool leader = (c < n) && __popc(m & ((1u << lane) - 1u)) == 0;
+    unsigned long long b = __ballot(leader);
+    unsigned elected = (unsigned)(b >> (t & 32));
+    if (c < n) {
+        unsigned lead = (unsigned)__ffs(m) - 1u;
+        int id = prefix[c >> 5] + __popc(elected & ((1u << lead) - 1u));
+        if (level == 0) {
+            cst0[c] = id;                       // m_CoarseSpaceTables[0][vid]
+            goingNext[c] = id + nv32;           // m_goingNext[vid]
+        } else {
+            masks[c] = (unsigned)id;            // m_nextConnectMsk[vid] := local id
+            goingNext[begin + c] = id + begin + ((n + 31) / 32) * 32;
+        }
+    }
+    if (c == 0) levelTotal[level + 1] = prefix[nBanks - 1] + counts[nBanks - 1];
+}
+
+// ComputeNextLevel, .cpp:1074-1084
+__global__ __launch_bounds__(256) void k_next_level(int nV, const int* __restrict__ cstPrev,
+                                                    const unsigned* __restrict__ ids, int* __restrict__ cstCur) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < nV) cstCur[v] = (int)ids[cstPrev[v]];
+}
+
+// AggregationKernel, .cpp:1092-1162, plus the per-vertex apply record
+// vmap[v] = {s2o[v], ancestor ids at levels 1..3}.
+__global__ __launch_bounds__(256) void k_vertex_maps(int nV, int L, const int* __restrict__ s2o,
+                                                     const int* __restrict__ goingNext, int4* __restrict__ coarseTables,
+                                                     int4* __restrict__ vmap) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nV) return;
+    int a[4] = {0, 0, 0, 0};
+    int cur = v;
+    for (int l = 0; l < L - 1 && l < 4; ++l) {
+        cur = goingNext[cur];
+        a[l] = cur;
+    }
+    coarseTables[v] = make_int4(a[0], a[1], a[2], a[3]);
+    vmap[v] = make_int4(s2o[v], a[0], a[1], a[2]);
+}
+
+// ---------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------
+
+static int scan_counts(mas_context* h, const int* counts, int* prefix, int n, hipStream_t s) {
+    size_t tmp = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, counts, prefix, n, s);
+    int rc = ensure(h, h->cubTemp, tmp);
+    if (rc) return rc;
+    return hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, counts, prefix, n, s), "exclusive scan");
+}
+
+static int read_int(mas_context* h, const int* dptr, int* out, hipStream_t s) {
+    int rc = hip_check(h, hipMemcpyAsync(out, dptr, sizeof(int), hipMemcpyDeviceToHost, s), "D2H level total");
+    if (rc) return rc;
+    return hip_check(h, hipStreamSynchronize(s), "level sync");
+}
+
+int build_stencils(mas_context* h, const void* ef, const void* ee, const void* vf, const unsigned* efC,
+                   const unsigned* eeC, const unsigned* vfC, hipStream_t s) {
+    long long efNum = efC ? efC[h->nE] : 0, eeNum = eeC ? eeC[h->nE] : 0, vfNum = vfC ? vfC[h->nV] : 0;
+    long long total = efNum + eeNum + vfNum;
+    const long long maxStencil = (long long)h->nV * 32;  // .cpp:187-188
+    h->nStencil = 0;
+    if (total <= 0) return MAS_OK;
+    if ((efNum && !ef) || (eeNum && !ee) || (vfNum && !vf)) return fail(h, MAS_ERR_ARG, "contact records missing");
+    if ((efNum || eeNum) && !h->edges.p) return fail(h, MAS_ERR_ARG, "EF/EE contacts need m_edges");
+    if ((efNum || vfNum) && !h->faces.p) return fail(h, MAS_ERR_ARG, "EF/VF contacts need m_faces");
+    if (total > maxStencil) {
+        // .cpp:312-316: the reference truncates and prints
+        std::fprintf(stderr, "stencil size %lld exceed max stencils num  %lld\n", total, maxStencil);
+        total = maxStencil;
+        if (efNum > total) efNum = total;
+        if (efNum + eeNum > total) eeNum = total - efNum;
+        vfNum = total - efNum - eeNum;
+    }
+    int rc;
+    if ((rc = ensure(h, h->rawContacts, (size_t)total * 48)) || (rc = ensure(h, h->stencilFlags, (size_t)total * 4)) ||
+        (rc = ensure(h, h->stencilSlots, (size_t)total * 4 + 16)) ||
+        (rc = ensure(h, h->stencils, (size_t)total * sizeof(DevStencil))))
+        return rc;
+    unsigned char* raw = P<unsigned char>(h->rawContacts);
+    if (efNum && (rc = hip_check(h, hipMemcpyAsync(raw, ef, efNum * 48, hipMemcpyHostToDevice, s), "H2D ef"))) return rc;
+    if (eeNum && (rc = hip_check(h, hipMemcpyAsync(raw + efNum * 48, ee, eeNum * 48, hipMemcpyHostToDevice, s), "H2D ee")))
+        return rc;
+    if (vfNum && (rc = hip_check(h, hipMemcpyAsync(raw + (efNum + eeNum) * 48, vf, vfNum * 48, hipMemcpyHostToDevice, s),
+                                 "H2D vf")))
+        return rc;
+    const int n = (int)total;
+    k_stencil_flags<<<cdiv(n, 256), 256, 0, s>>>(raw, (int)efNum, (int)eeNum, n, h->nV, h->nE, h->nF,
+                                                 P<int>(h->stencilFlags));
+    std::vector<int> flags(n);
+    if ((rc = hip_check(h, hipMemcpyAsync(flags.data(), h->stencilFlags.p, (size_t)n * 4, hipMemcpyDeviceToHost, s),
+                        "D2H flags")) ||
+        (rc = hip_check(h, hipStreamSynchronize(s), "flags sync")))
+        return rc;
+    int valid = 0;
+    for (int f : flags) {
+        if (f == 2) return fail(h, MAS_ERR_ARG, "contact record references an out-of-range edge/face/vertex");
+        valid += (f == 1);
+    }
+    // deterministic compaction == the reference's atomic slot counter at CPU_THREAD_NUM=1
+    if ((rc = scan_counts(h, P<int>(h->stencilFlags), P<int>(h->stencilSlots), n, s))) return rc;
+    k_stencil_build<<<cdiv(n, 256), 256, 0, s>>>(raw, (int)efNum, (int)eeNum, n, P<int>(h->stencilFlags),
+                                                 P<int>(h->stencilSlots), P<int4>(h->edges), P<int4>(h->faces),
+                                                 P<int>(h->o2s), h->cfg.fix_vf_bary, P<DevStencil>(h->stencils));
+    h->nStencil = valid;
+    return hip_check(h, hipGetLastError(), "stencil kernels");
+}
+
+// ReorderRealtime, .cpp:415-445
+int run_levels(mas_context* h, hipStream_t s) {
+    const int nV = h->nV, L = h->L, nv32 = ceil32(nV);
+    const int nB0 = nv32 / 32;
+    int rc;
+    if ((rc = ensure(h, h->fineMask, (size_t)nv32 * 4)) || (rc = ensure(h, h->nextMask, (size_t)nv32 * 4)) ||
+        (rc = ensure(h, h->bankCount, (size_t)(nB0 + 1) * 4)) || (rc = ensure(h, h->bankPrefix, (size_t)(nB0 + 1) * 4)) ||
+        (rc = ensure(h, h->levelTotal, 16 * 4)) || (rc = ensure(h, h->cst, (size_t)L * nV * 4)) ||
+        (rc = ensure(h, h->goingNext, (size_t)(L + 1) * nv32 * 4)) || (rc = ensure(h, h->vmap, (size_t)nV * 16)) ||
+        (rc = ensure(h, h->coarseTables, (size_t)nV * 16)))
+        return rc;
+    std::fill(h->levelSize, h->levelSize + 18, 0);
+    int* cst = P<int>(h->cst);
+    int* gn = P<int>(h->goingNext);
+    unsigned* fine = P<unsigned>(h->fineMask);
+    unsigned* next = P<unsigned>(h->nextMask);
+    int* cnt = P<int>(h->bankCount);
+    int* pre = P<int>(h->bankPrefix);
+    int* tot = P<int>(h->levelTotal);
+    const DevStencil* st = P<DevStencil>(h->stencils);
+    const int g = cdiv(nV, 256);
+    if ((rc = hip_check(h, hipMemsetAsync(gn, 0, (size_t)(L + 1) * nv32 * 4, s), "memset goingNext"))) return rc;
+
+    // level 0 -> 1
+    k_connect_l0<<<g, 256, 0, s>>>(nV, P<int>(h->nbrNumRem), P<int>(h->nbrRem), fine);
+    if (h->nStencil) k_collision_connect<<<cdiv(h->nStencil, 256), 256, 0, s>>>(st, h->nStencil, nullptr, fine);
+    k_bank_closure<<<cdiv(nV, 256), 256, 0, s>>>(nV, fine, cnt);
+    if ((rc = scan_counts(h, cnt, pre, nB0, s))) return rc;
+    k_assign_ids<<<cdiv(nV, 256), 256, 0, s>>>(nV, 0, 0, nv32, fine, pre, cnt, nB0, cst, gn, tot);
+    int total = 0;
+    if ((rc = read_int(h, tot + 1, &total, s))) return rc;
+    h->levelSize[2] = total;
+    h->levelSize[3] = nv32;
+
+    for (int level = 1; level < L; ++level) {  // .cpp:427-440
+        const int n = h->levelSize[2 * level], begin = h->levelSize[2 * level + 1];
+        const int nb = cdiv(n, 32);
+        const int* prev = cst + (size_t)(level - 1) * nV;
+        if ((rc = hip_check(h, hipMemsetAsync(next, 0, (size_t)nv32 * 4, s), "memset nextMask"))) return rc;
+        k_connect_lx<<<g, 256, 0, s>>>(nV, prev, P<int>(h->nbrNumRem), P<int>(h->nbrRem), next);
+        if (h->nStencil) k_collision_connect<<<cdiv(h->nStencil, 256), 256, 0, s>>>(st, h->nStencil, prev, next);
+        k_bank_closure<<<cdiv(n, 256), 256, 0, s>>>(n, next, cnt);
+        if ((rc = scan_counts(h, cnt, pre, nb, s))) return rc;
+        k_assign_ids<<<cdiv(n, 256), 256, 0, s>>>(n, level, begin, nv32, next, pre, cnt, nb, nullptr, gn, tot);
+        k_next_level<<<g, 256, 0, s>>>(nV, prev, next, cst + (size_t)level * nV);
+        if ((rc = read_int(h, tot + level + 1, &total, s))) return rc;
+        h->levelSize[2 * (level + 1)] = total;
+        h->levelSize[2 * (level + 1) + 1] = begin + ceil32(n);
+    }
+    h->totalClusters = h->levelSize[2 * L + 1];  // TotalNodes, .cpp:1086-1090
+    h->nBlk = h->totalClusters / 32;
+    h->nFineBlk = nv32 / 32;
+    k_vertex_maps<<<g, 256, 0, s>>>(nV, L, P<int>(h->s2o), gn, P<int4>(h->coarseTables), P<int4>(h->vmap));
+    return hip_check(h, hipGetLastError(), "level kernels");
+}
+
+}  // namespace mas

@@ -1,0 +1,288 @@
+// mas_capi.hip -- C ABI entry points (include/mas_capi.h) and shared helpers.
+//
+// The handle owns every device buffer; all work is enqueued on one HIP stream.
+// Host-pointer entry points stage through device buffers and synchronise, so a
+// PCG loop that calls the reference's three methods keeps working unchanged
+// (SeSchwarzPreconditioner.h:56-63).
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "mas_internal.h"
+
+namespace mas {
+
+int fail(mas_context* h, int code, const std::string& msg) {
+    if (h) h->err = msg;
+    return code;
+}
+
+int hip_check(mas_context* h, hipError_t e, const char* what) {
+    if (e == hipSuccess) return MAS_OK;
+    return fail(h, MAS_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int ensure(mas_context* h, Buffer& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return MAS_OK;
+    if (b.p) {
+        hipStreamSynchronize(h->stream);
+        hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return fail(h, MAS_ERR_NOMEM, std::string("hipMalloc ") + std::to_string(bytes) + " B: " + hipGetErrorString(e));
+    }
+    b.bytes = bytes;
+    return MAS_OK;
+}
+
+static void release(Buffer& b) {
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+}  // namespace mas
+
+using namespace mas;
+
+#define MAS_TRY(x)                 \
+    do {                           \
+        int _rc = (x);             \
+        if (_rc != MAS_OK) return _rc; \
+    } while (0)
+
+extern "C" {
+
+int mas_version(void) { return MAS_ABI_VERSION; }
+
+int mas_create(mas_handle* out, const mas_config* cfg) {
+    if (!out) return MAS_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MAS_ERR_NO_DEVICE;
+    mas_context* h = new (std::nothrow) mas_context();
+    if (!h) return MAS_ERR_NOMEM;
+    if (cfg) h->cfg = *cfg;
+    else h->cfg.device = -1;
+    if (h->cfg.max_levels < 0 || h->cfg.resort_period < 0) {
+        delete h;
+        return MAS_ERR_ARG;
+    }
+    if (h->cfg.device >= 0) {
+        if (h->cfg.device >= ndev || hipSetDevice(h->cfg.device) != hipSuccess) {
+            delete h;
+            return MAS_ERR_ARG;
+        }
+        h->device = h->cfg.device;
+    } else {
+        hipGetDevice(&h->device);
+    }
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return MAS_ERR_HIP;
+    }
+    for (auto& e : h->ev) hipEventCreate(&e);
+    int rc = upload_slot_table(h);
+    if (rc != MAS_OK) {
+        mas_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return MAS_OK;
+}
+
+int mas_destroy(mas_handle h) {
+    if (!h) return MAS_ERR_ARG;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    h->for_each_buffer([](Buffer& b) { release(b); });
+    for (auto& e : h->ev)
+        if (e) hipEventDestroy(e);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return MAS_OK;
+}
+
+const char* mas_last_error(mas_handle h) { return h ? h->err.c_str() : "null handle"; }
+
+int mas_allocate(mas_handle h, int nV, int nE, int nF, const float* pos4, const int* nbr_starts, const int* nbr_idx,
+                 const int* edges4, const int* faces4) {
+    if (!h) return MAS_ERR_ARG;
+    if (nV <= 0 || nE < 0 || nF < 0 || !pos4 || !nbr_starts || !nbr_idx)
+        return fail(h, MAS_ERR_ARG, "mas_allocate: bad arguments");
+    if (h->allocated && nV != h->nV)
+        return fail(h, MAS_ERR_STATE, "mas_allocate: numVerts must stay fixed after the first call");
+    hipSetDevice(h->device);
+    h->nE = nE;
+    h->nF = nF;
+    h->nV = nV;
+    return run_allocate(h, pos4, nbr_starts, nbr_idx, edges4, faces4);
+}
+
+static int prepare_common(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges, const void* ef,
+                          const void* ee, const void* vf, const unsigned* efC, const unsigned* eeC,
+                          const unsigned* vfC, hipStream_t s) {
+    if (!h->allocated) return fail(h, MAS_ERR_STATE, "prepare before allocate");
+    return run_prepare(h, d_diag9, d_off9, d_ranges, ef, ee, vf, efC, eeC, vfC, s);
+}
+
+int mas_prepare(mas_handle h, const float* diag9, const float* off9, const int* ranges, const void* ef, const void* ee,
+                const void* vf, const unsigned* efC, const unsigned* eeC, const unsigned* vfC) {
+    if (!h) return MAS_ERR_ARG;
+    if (!diag9 || !off9 || !ranges) return fail(h, MAS_ERR_ARG, "mas_prepare: null Hessian pointer");
+    if (!h->allocated) return fail(h, MAS_ERR_STATE, "prepare before allocate");
+    hipSetDevice(h->device);
+    const size_t nV = h->nV, nnz = h->nnz;
+    MAS_TRY(ensure(h, h->diagStage, nV * 36));
+    MAS_TRY(ensure(h, h->offStage, nnz * 36));
+    MAS_TRY(ensure(h, h->rangeStage, (nV + 1) * 4));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(h->diagStage.p, diag9, nV * 36, hipMemcpyHostToDevice, h->stream), "H2D diag"));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(h->offStage.p, off9, nnz * 36, hipMemcpyHostToDevice, h->stream), "H2D off"));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(h->rangeStage.p, ranges, (nV + 1) * 4, hipMemcpyHostToDevice, h->stream),
+                      "H2D ranges"));
+    MAS_TRY(prepare_common(h, P<float>(h->diagStage), P<float>(h->offStage), P<int>(h->rangeStage), ef, ee, vf, efC,
+                           eeC, vfC, h->stream));
+    return hip_check(h, hipStreamSynchronize(h->stream), "prepare sync");
+}
+
+int mas_prepare_device(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges, const void* ef,
+                       const void* ee, const void* vf, const unsigned* efC, const unsigned* eeC, const unsigned* vfC,
+                       void* stream) {
+    if (!h) return MAS_ERR_ARG;
+    if (!d_diag9 || !d_off9 || !d_ranges) return fail(h, MAS_ERR_ARG, "mas_prepare_device: null Hessian pointer");
+    hipSetDevice(h->device);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    return prepare_common(h, d_diag9, d_off9, d_ranges, ef, ee, vf, efC, eeC, vfC, s);
+}
+
+int mas_apply_device(mas_handle h, float* d_z4, const float* d_r4, void* stream) {
+    if (!h) return MAS_ERR_ARG;
+    if (!d_z4 || !d_r4) return fail(h, MAS_ERR_ARG, "mas_apply_device: null vector");
+    if ((reinterpret_cast<uintptr_t>(d_z4) | reinterpret_cast<uintptr_t>(d_r4)) & 15)
+        return fail(h, MAS_ERR_ARG, "mas_apply_device: vectors must be 16-byte aligned");
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    return run_apply(h, reinterpret_cast<float4*>(d_z4), reinterpret_cast<const float4*>(d_r4), s);
+}
+
+int mas_apply(mas_handle h, float* z4, const float* r4) {
+    if (!h) return MAS_ERR_ARG;
+    if (!z4 || !r4) return fail(h, MAS_ERR_ARG, "mas_apply: null vector");
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    hipSetDevice(h->device);
+    const size_t bytes = (size_t)h->nV * 16;
+    MAS_TRY(ensure(h, h->rStage, bytes));
+    MAS_TRY(ensure(h, h->zStage, bytes));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(h->rStage.p, r4, bytes, hipMemcpyHostToDevice, h->stream), "H2D r"));
+    MAS_TRY(run_apply(h, P<float4>(h->zStage), P<float4>(h->rStage), h->stream));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(z4, h->zStage.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H z"));
+    return hip_check(h, hipStreamSynchronize(h->stream), "apply sync");
+}
+
+int mas_set_profiling(mas_handle h, int enable) {
+    if (!h) return MAS_ERR_ARG;
+    h->profiling = enable != 0;
+    return MAS_OK;
+}
+
+int mas_get_info(mas_handle h, mas_info* out) {
+    if (!h || !out) return MAS_ERR_ARG;
+    std::memset(out, 0, sizeof(*out));
+    out->num_verts = h->nV;
+    out->num_edges = h->nE;
+    out->num_faces = h->nF;
+    out->num_levels = h->L;
+    out->natural_levels = h->natL;
+    out->total_clusters = h->totalClusters;
+    out->num_blocks = h->nBlk;
+    out->num_fine_blocks = h->nFineBlk;
+    out->max_neighbors = h->maxNbr;
+    out->num_stencils = h->nStencil;
+    std::memcpy(out->level_size, h->levelSize, sizeof(out->level_size));
+    out->inv_bytes = (int64_t)h->nBlk * kBlockFloats * 4;
+    h->for_each_buffer([&](Buffer& b) { out->device_bytes += (int64_t)b.bytes; });
+    return MAS_OK;
+}
+
+int mas_get_stats(mas_handle h, mas_stats* out) {
+    if (!h || !out) return MAS_ERR_ARG;
+    if (h->profiling && h->stats.apply_calls > 0) {
+        hipEventSynchronize(h->ev[9]);
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, h->ev[4], h->ev[5]) == hipSuccess) h->stats.apply_restrict_ms = t;
+        if (hipEventElapsedTime(&t, h->ev[6], h->ev[7]) == hipSuccess) h->stats.apply_coarse_ms = t;
+        if (hipEventElapsedTime(&t, h->ev[8], h->ev[9]) == hipSuccess) h->stats.apply_fine_ms = t;
+        if (hipEventElapsedTime(&t, h->ev[4], h->ev[9]) == hipSuccess) h->stats.apply_ms = t;
+    }
+    *out = h->stats;
+    return MAS_OK;
+}
+
+int mas_get_maps(mas_handle h, uint64_t* morton, int* s2o, int* o2s, int* cst, int* going_next, int* coarse_tables,
+                 unsigned* fine_mask) {
+    if (!h) return MAS_ERR_ARG;
+    if (!h->allocated) return fail(h, MAS_ERR_STATE, "maps before allocate");
+    hipSetDevice(h->device);
+    hipStreamSynchronize(h->stream);
+    const size_t nV = h->nV;
+    auto cp = [&](void* dst, const Buffer& b, size_t bytes) -> int {
+        if (!dst) return MAS_OK;
+        if (!b.p || b.bytes < bytes) return fail(h, MAS_ERR_STATE, "map not computed yet");
+        return hip_check(h, hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost), "D2H maps");
+    };
+    MAS_TRY(cp(morton, h->morton, nV * 8));
+    MAS_TRY(cp(s2o, h->s2o, nV * 4));
+    MAS_TRY(cp(o2s, h->o2s, nV * 4));
+    if (cst || going_next || coarse_tables || fine_mask) {
+        if (!h->prepared) return fail(h, MAS_ERR_STATE, "level maps before prepare");
+        MAS_TRY(cp(cst, h->cst, (size_t)h->L * nV * 4));
+        MAS_TRY(cp(going_next, h->goingNext, (size_t)h->totalClusters * 4));
+        MAS_TRY(cp(coarse_tables, h->coarseTables, nV * 16));
+        MAS_TRY(cp(fine_mask, h->fineMask, nV * 4));
+    }
+    return MAS_OK;
+}
+
+int mas_get_neighbors(mas_handle h, int* nbr_num, int* nbr) {
+    if (!h) return MAS_ERR_ARG;
+    if (!h->allocated) return fail(h, MAS_ERR_STATE, "neighbors before allocate");
+    hipSetDevice(h->device);
+    hipStreamSynchronize(h->stream);
+    if (nbr_num) MAS_TRY(hip_check(h, hipMemcpy(nbr_num, h->nbrNum.p, (size_t)h->nV * 4, hipMemcpyDeviceToHost), "D2H"));
+    if (nbr)
+        MAS_TRY(hip_check(h, hipMemcpy(nbr, h->nbr.p, (size_t)h->maxNbr * h->nV * 4, hipMemcpyDeviceToHost), "D2H"));
+    return MAS_OK;
+}
+
+int mas_get_block_matrix(mas_handle h, int blk, float* out96) {
+    if (!h || !out96) return MAS_ERR_ARG;
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "block matrix before prepare");
+    if (blk < 0 || blk >= h->nBlk) return fail(h, MAS_ERR_ARG, "block index out of range");
+    hipSetDevice(h->device);
+    hipStreamSynchronize(h->stream);
+    MAS_TRY(hip_check(h, hipMemcpy(out96, P<float>(h->dense) + (size_t)blk * kDenseFloats, kDenseFloats * 4,
+                                   hipMemcpyDeviceToHost), "D2H block"));
+    // zero-diagonal -> identity rule (.cpp:1365-1368), as the factor kernel applies it
+    for (int x = 0; x < 32; ++x) {
+        if (out96[(3 * x) * 96 + 3 * x] != 0.0f) continue;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) out96[(3 * x + i) * 96 + 3 * x + j] = (i == j) ? 1.f : 0.f;
+    }
+    return MAS_OK;
+}
+
+int mas_get_block_inverse(mas_handle h, int blk, float* out96) {
+    if (!h || !out96) return MAS_ERR_ARG;
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "block inverse before prepare");
+    if (blk < 0 || blk >= h->nBlk) return fail(h, MAS_ERR_ARG, "block index out of range");
+    hipSetDevice(h->device);
+    hipStreamSynchronize(h->stream);
+    return copy_block_inverse(h, blk, out96);
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+// mas_internal.h -- device-side state of one MAS preconditioner handle.
+//
+// Data layout in HBM (DESIGN.md "Data layout"):
+//   * node ids follow the reference numbering: level 0 =
+//     Morton-sorted vertices [0, ceil32(nV)), level l >= 1 at
+//     [begin_l, begin_l + ceil32(n_l)), total_clusters = begin_L.  A 32-node
+//     "bank" is one Schwarz subdomain block; block b = nodes [32b, 32b+32).
+//   * vmap[v] (int4, per sorted vertex) = {s2o[v], a1, a2, a3}: the original
+//     id and the global ids of the level-1..3 ancestors -- everything the fine
+//     apply kernel needs about a vertex in one 16-byte load.
+//   * inv: per block 4656 fp32 (18 624 B, the reference's packed size) in the
+//     node-pair-rotation layout described in k_apply.hip.
+//   * Rc / Zc: coarse residual / solution, float4 per node id >= begin_1.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/mas_capi.h"
+
+namespace mas {
+
+constexpr int kBank = 32;
+constexpr int kBlockFloats = 4656;      // (96*97)/2 packed symmetric 96x96
+constexpr int kBlockF4 = kBlockFloats / 4;  // 1164 float4 per block
+constexpr int kMaxLevels = 5;             // reference B-6
+constexpr int kDenseFloats = 96 * 96;
+
+// Stencil, SeCollisionElements.h:60-69 (device copy; direction xyz only).
+struct DevStencil {
+    int n, nFirst;
+    int idx[5];     // sorted (mapped) vertex ids, MapCollisionStencilIndices .cpp:287-302
+    float w[5];
+    float stiff;
+    float dir[3];
+};
+
+struct Buffer {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace mas
+
+struct mas_context {
+    mas_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // sizes
+    int nV = 0, nE = 0, nF = 0, nnz = 0;
+    int natL = 0, L = 0, maxNbr = 0;
+    int allocCalls = 0;   // reference m_frameIndex semantics (B-1)
+    bool allocated = false, prepared = false, profiling = false;
+    int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
+    int levelSize[2 * 9] = {};
+
+    // allocate-phase device data
+    mas::Buffer pos, starts, idx, edges, faces;
+    mas::Buffer morton, mortonSorted, iota, s2o, o2s;
+    mas::Buffer nbrNum, nbr, nbrNumRem, nbrRem;
+    mas::Buffer aabbPartial;
+    // prepare-phase device data
+    mas::Buffer rawContacts, stencilFlags, stencilSlots, stencils;
+    mas::Buffer fineMask, nextMask, bankCount, bankPrefix, levelTotal;
+    mas::Buffer cst, goingNext, vmap, coarseTables;
+    mas::Buffer dense, inv, slotTable;
+    mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
+    mas::Buffer vkeys, vlist, voff, tab;
+    mas::Buffer Rc, Zc;
+    // staging for host-pointer entry points
+    mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
+    // hipcub scratch
+    mas::Buffer cubTemp;
+    // events: [0..1] allocate, [2..3] prepare, [4..9] apply kernels
+    hipEvent_t ev[12] = {};
+    mas_stats stats{};
+
+    template <class F>
+    void for_each_buffer(F f) {
+        mas::Buffer* all[] = {&pos, &starts, &idx, &edges, &faces, &morton, &mortonSorted, &iota, &s2o, &o2s,
+                              &nbrNum, &nbr, &nbrNumRem, &nbrRem, &aabbPartial, &rawContacts, &stencilFlags,
+                              &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
+                              &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &additional, &od,
+                              &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
+                              &vlist, &voff, &tab, &Rc, &Zc, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &cubTemp};
+        for (mas::Buffer* b : all) f(*b);
+    }
+};
+
+// ---- helpers shared by the .hip translation units ----
+namespace mas {
+
+int fail(mas_context* h, int code, const std::string& msg);
+int hip_check(mas_context* h, hipError_t e, const char* what);
+int ensure(mas_context* h, Buffer& b, size_t bytes);
+template <class T>
+inline T* P(Buffer& b) { return reinterpret_cast<T*>(b.p); }
+template <class T>
+inline const T* P(const Buffer& b) { return reinterpret_cast<const T*>(b.p); }
+inline int ceil32(int x) { return (x + 31) / 32 * 32; }
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// phase entry points (host orchestration), defined per translation unit
+int run_allocate(mas_context* h, const float* pos4, const int* starts, const int* idx, const int* edges4,
+                 const int* faces4);
+int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, const void* ef,
+                const void* ee, const void* vf, const unsigned* efC, const unsigned* eeC, const unsigned* vfC,
+                hipStream_t s);
+int build_stencils(mas_context* h, const void* ef, const void* ee, const void* vf, const unsigned* efC,
+                   const unsigned* eeC, const unsigned* vfC, hipStream_t s);
+int run_levels(mas_context* h, hipStream_t s);
+int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s);
+int run_factor(mas_context* h, hipStream_t s);
+int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s);
+int upload_slot_table(mas_context* h);
+int copy_block_inverse(mas_context* h, int blk, float* out96);
+
+}  // namespace mas

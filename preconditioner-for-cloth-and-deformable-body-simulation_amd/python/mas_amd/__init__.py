@@ -1,0 +1,236 @@
+"""Python binding of the MI355X MAS preconditioner C ABI (include/mas_capi.h).
+
+Mirrors the reference plugin surface (SeSchwarzPreconditioner.h:37-178):
+
+    P = SeSchwarzPreconditioner(max_levels=4)
+    P.m_positions, P.m_neighbours, P.m_edges, P.m_faces = ...
+    P.AllocatePrecoditioner(nV, nE, nF)
+    P.PreparePreconditioner(diag, off, ranges, ef, ee, vf, efC, eeC, vfC)
+    z = P.Preconditioning(None, r, 3 * nV)        # host arrays
+    P.PreconditioningDevice(z_dev, r_dev, stream) # torch cuda tensors / raw pointers
+
+The shared library is loaded from the package's lib/ directory; there is no
+CPU fallback -- if the HIP library or a GPU is missing every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmas_amd.so")
+FACADE_PATH = os.path.join(LIB_DIR, "libSeSchwarzPreconditioner.so")
+
+MAS_OK = 0
+STATUS = {0: "MAS_OK", -1: "MAS_ERR_ARG", -2: "MAS_ERR_HIP", -3: "MAS_ERR_CAPACITY", -4: "MAS_ERR_STATE",
+          -5: "MAS_ERR_LEVELS", -6: "MAS_ERR_NOMEM", -7: "MAS_ERR_NO_DEVICE"}
+
+# every entry point declared in include/mas_capi.h
+EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_allocate", "mas_prepare",
+           "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_get_info",
+           "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse"]
+
+
+class mas_config(ctypes.Structure):
+    _fields_ = [("max_levels", ctypes.c_int), ("resort_period", ctypes.c_int), ("fix_vf_bary", ctypes.c_int),
+                ("device", ctypes.c_int), ("reserved", ctypes.c_int * 12)]
+
+
+class mas_info(ctypes.Structure):
+    _fields_ = [("num_verts", ctypes.c_int), ("num_edges", ctypes.c_int), ("num_faces", ctypes.c_int),
+                ("num_levels", ctypes.c_int), ("natural_levels", ctypes.c_int), ("total_clusters", ctypes.c_int),
+                ("num_blocks", ctypes.c_int), ("num_fine_blocks", ctypes.c_int), ("max_neighbors", ctypes.c_int),
+                ("num_stencils", ctypes.c_int), ("level_size", ctypes.c_int * 18), ("inv_bytes", ctypes.c_int64),
+                ("device_bytes", ctypes.c_int64)]
+
+
+class mas_stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in ("allocate_ms", "prepare_ms", "apply_ms", "prepare_levels_ms",
+                                               "prepare_assemble_ms", "prepare_factor_ms", "apply_restrict_ms",
+                                               "apply_coarse_ms", "apply_fine_ms")] + [("apply_calls", ctypes.c_int64)]
+
+
+class MasError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libmas_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MasError(f"{LIB_PATH} not found: run `make -C {PKG_ROOT}` (or __graft_entry__.build())")
+        # torch-ROCm ships its own libamdhip64.so.7 / libhsa-runtime64.so.  Load
+        # torch first so libmas_amd.so binds to the same HIP runtime (same
+        # soname) and device pointers can be shared with torch tensors.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        P, I = ctypes.c_void_p, ctypes.c_int
+        L.mas_version.restype = I
+        L.mas_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(mas_config)]
+        L.mas_destroy.argtypes = [P]
+        L.mas_last_error.argtypes = [P]
+        L.mas_last_error.restype = ctypes.c_char_p
+        L.mas_allocate.argtypes = [P, I, I, I, P, P, P, P, P]
+        L.mas_prepare.argtypes = [P, P, P, P, P, P, P, P, P, P]
+        L.mas_prepare_device.argtypes = [P, P, P, P, P, P, P, P, P, P, P]
+        L.mas_apply.argtypes = [P, P, P]
+        L.mas_apply_device.argtypes = [P, P, P, P]
+        L.mas_set_profiling.argtypes = [P, I]
+        L.mas_get_info.argtypes = [P, ctypes.POINTER(mas_info)]
+        L.mas_get_stats.argtypes = [P, ctypes.POINTER(mas_stats)]
+        L.mas_get_maps.argtypes = [P, P, P, P, P, P, P, P]
+        L.mas_get_neighbors.argtypes = [P, P, P]
+        L.mas_get_block_matrix.argtypes = [P, I, P]
+        L.mas_get_block_inverse.argtypes = [P, I, P]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    if hasattr(a, "data_ptr"):  # torch tensor
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dtype):
+    return None if a is None else np.ascontiguousarray(a, dtype=dtype)
+
+
+class SeSchwarzPreconditioner:
+    """Reference-compatible surface (SE::SeSchwarzPreconditioner) on the GPU."""
+
+    def __init__(self, max_levels: int = 0, resort_period: int = 0, fix_vf_bary: bool = False, device: int = -1):
+        self._L = lib()
+        cfg = mas_config(max_levels, resort_period, int(fix_vf_bary), device)
+        h = ctypes.c_void_p()
+        rc = self._L.mas_create(ctypes.byref(h), ctypes.byref(cfg))
+        if rc != MAS_OK:
+            raise MasError(f"mas_create failed: {STATUS.get(rc, rc)}")
+        self.h = h
+        self.m_positions = None   # [nV, 4] float32
+        self.m_edges = None       # [nE, 4] int32
+        self.m_faces = None       # [nF, 4] int32
+        self.m_neighbours = None  # (starts, idx) CSR
+        self._keep = ()
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            self._L.mas_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def _check(self, rc, what):
+        if rc != MAS_OK:
+            msg = self._L.mas_last_error(self.h)
+            raise MasError(f"{what} failed: {STATUS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    # ---- the reference's three methods ----
+    def AllocatePrecoditioner(self, numVerts, numEdges, numFaces):
+        starts, idx = self.m_neighbours
+        pos = _c(self.m_positions, np.float32)
+        starts = _c(starts, np.int32)
+        idx = _c(idx, np.int32)
+        edges = _c(self.m_edges, np.int32)
+        faces = _c(self.m_faces, np.int32)
+        self._check(self._L.mas_allocate(self.h, numVerts, numEdges, numFaces, _ptr(pos), _ptr(starts), _ptr(idx),
+                                         _ptr(edges), _ptr(faces)), "AllocatePrecoditioner")
+
+    AllocatePreconditioner = AllocatePrecoditioner
+
+    def PreparePreconditioner(self, diagonal, csrOffDiagonals, csrRanges, efSets=None, eeSets=None, vfSets=None,
+                              efCounts=None, eeCounts=None, vfCounts=None):
+        d = _c(diagonal, np.float32)
+        o = _c(csrOffDiagonals, np.float32)
+        r = _c(csrRanges, np.int32)
+        efC, eeC, vfC = (_c(x, np.uint32) for x in (efCounts, eeCounts, vfCounts))
+        self._check(self._L.mas_prepare(self.h, _ptr(d), _ptr(o), _ptr(r), _ptr(efSets), _ptr(eeSets), _ptr(vfSets),
+                                        _ptr(efC), _ptr(eeC), _ptr(vfC)), "PreparePreconditioner")
+
+    def PreparePreconditionerDevice(self, d_diag, d_off, d_ranges, efSets=None, eeSets=None, vfSets=None,
+                                    efCounts=None, eeCounts=None, vfCounts=None, stream=None):
+        efC, eeC, vfC = (_c(x, np.uint32) for x in (efCounts, eeCounts, vfCounts))
+        self._check(self._L.mas_prepare_device(self.h, _ptr(d_diag), _ptr(d_off), _ptr(d_ranges), _ptr(efSets),
+                                               _ptr(eeSets), _ptr(vfSets), _ptr(efC), _ptr(eeC), _ptr(vfC),
+                                               _ptr(stream)), "PreparePreconditionerDevice")
+
+    def Preconditioning(self, z, residual, dim=None):
+        r = _c(residual, np.float32)
+        out = np.empty_like(r) if z is None else z
+        self._check(self._L.mas_apply(self.h, _ptr(out), _ptr(r)), "Preconditioning")
+        return out
+
+    def PreconditioningDevice(self, z, residual, stream=None):
+        """z, residual: torch cuda float32 tensors [nV, 4] (or raw device pointers)."""
+        self._check(self._L.mas_apply_device(self.h, _ptr(z), _ptr(residual), _ptr(stream)), "PreconditioningDevice")
+
+    # ---- introspection ----
+    def set_profiling(self, on: bool):
+        self._check(self._L.mas_set_profiling(self.h, int(on)), "set_profiling")
+
+    def info(self) -> dict:
+        i = mas_info()
+        self._check(self._L.mas_get_info(self.h, ctypes.byref(i)), "get_info")
+        d = {k: getattr(i, k) for k, _ in mas_info._fields_ if k != "level_size"}
+        d["level_size"] = np.array(i.level_size[: 2 * (i.num_levels + 1)], dtype=np.int32).reshape(-1, 2)
+        return d
+
+    def stats(self) -> dict:
+        s = mas_stats()
+        self._check(self._L.mas_get_stats(self.h, ctypes.byref(s)), "get_stats")
+        return {k: getattr(s, k) for k, _ in mas_stats._fields_}
+
+    def maps(self) -> dict:
+        inf = self.info()
+        nV, L, tc = inf["num_verts"], inf["num_levels"], inf["total_clusters"]
+        out = dict(morton=np.zeros(nV, np.uint64), s2o=np.zeros(nV, np.int32), o2s=np.zeros(nV, np.int32),
+                   coarse_space_tables=np.zeros((L, nV), np.int32), going_next=np.zeros(tc, np.int32),
+                   coarse_tables=np.zeros((nV, 4), np.int32), fine_connect_mask=np.zeros(nV, np.uint32))
+        self._check(self._L.mas_get_maps(self.h, *[_ptr(out[k]) for k in ("morton", "s2o", "o2s",
+                                                                          "coarse_space_tables", "going_next",
+                                                                          "coarse_tables", "fine_connect_mask")]),
+                    "get_maps")
+        mx = inf["max_neighbors"]
+        out["nbr_num"] = np.zeros(nV, np.int32)
+        out["nbr"] = np.zeros((mx, nV), np.int32)
+        self._check(self._L.mas_get_neighbors(self.h, _ptr(out["nbr_num"]), _ptr(out["nbr"])), "get_neighbors")
+        out["level_size"] = inf["level_size"]
+        return out
+
+    def block_matrix(self, blk):
+        A = np.zeros((96, 96), np.float32)
+        self._check(self._L.mas_get_block_matrix(self.h, blk, _ptr(A)), "get_block_matrix")
+        return A
+
+    def block_inverse(self, blk):
+        B = np.zeros((96, 96), np.float32)
+        self._check(self._L.mas_get_block_inverse(self.h, blk, _ptr(B)), "get_block_inverse")
+        return B
+
+
+def from_mesh(mesh, max_levels=0, contacts=None, **kw) -> SeSchwarzPreconditioner:
+    """Allocate + Prepare a preconditioner for a meshgen.Mesh (host path)."""
+    P = SeSchwarzPreconditioner(max_levels=max_levels, **kw)
+    P.m_positions = mesh.pos
+    P.m_neighbours = (mesh.starts, mesh.idx)
+    P.m_edges = mesh.edges
+    P.m_faces = mesh.faces
+    P.AllocatePrecoditioner(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0])
+    if contacts is None:
+        P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
+    else:
+        vf, vfC = contacts
+        P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, vf, None, None, vfC)
+    return P
