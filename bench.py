@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""bench.py -- MAS preconditioner apply throughput on MI355X.
+
+One "step" = one Preconditioning apply (SeSchwarzPreconditioner.cpp:100-110)
+of the benchmark workload on device-resident r / z (float4 [nV], the
+SeVec3fSimd layout), after Allocate + Prepare.  Default workload: BASELINE.json
+configs[2], the 1M-vertex cloth Hessian (1024 x 1024 grid) + 100k VF contact
+stencils, 4 levels, 32-node subdomains, fp32 -- the configuration the north
+star's 1-GPU roofline target is quoted on.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): every rank runs
+the full workload on its own GPU ("replicas"; weak scaling) -- see DESIGN.md
+"Multi-GPU" for the sharded path.  Rank 0 prints ONE JSON line.
+
+roofline: the dominant kernel is the fused fine-level kernel (gather r through
+the Morton map, 32-node block solves, prolongation, scatter z).  Its
+algorithmic bytes per launch = nFineBlocks * 18 624 B (packed fp32 inverse,
+SURVEY §8(d)) + nV * (16 r + 16 z + 4 perm + 4 * (min(L,4)-1) ancestor ids);
+its average duration comes from HIP events the library records on the apply
+stream around that kernel during the timed steps.
+
+cpu_baseline: the CPU restatement of the reference (oracle/, OpenMP, the
+reference's packed layout and loop structure) on this host, bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "preconditioner-for-cloth-and-deformable-body-simulation_amd")
+sys.path.insert(0, os.path.join(PKG, "python"))
+
+METRIC = "preconditioner applies/sec + ms/apply, N-vertex 3×3-block cloth Hessian"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CONFIG_ORDER = ["10k", "256k", "1M+contacts", "1M", "4M-tet"]   # BASELINE.json configs order
+BLOCK_BYTES = 4656 * 4
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(info):
+    nV, L = info["num_verts"], info["num_levels"]
+    per_vertex = 16 + 16 + 4 + 4 * (min(L, 4) - 1)
+    fine = info["num_fine_blocks"] * BLOCK_BYTES + nV * per_vertex
+    apply = info["num_blocks"] * BLOCK_BYTES + nV * per_vertex
+    return fine, apply
+
+
+def cpu_baseline(mesh, cfg, contacts, r_np, steps):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from oracle import Oracle  # test infrastructure: the timed CPU baseline only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or max(1, (os.cpu_count() or 2) - 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], cfg["levels"], threads)
+    o.allocate(mesh)
+    if contacts is None:
+        o.prepare(mesh)
+    else:
+        o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
+    for _ in range(3):
+        o.apply(r_np)
+    ts = []
+    for _ in range(steps):
+        t = time.perf_counter()
+        z = o.apply(r_np)
+        ts.append(time.perf_counter() - t)
+    med = statistics.median(ts)
+    return {"value": round(1.0 / med, 3), "unit": "applies/s", "cores": threads, "kind": "port",
+            "sample": f"{cfg['name']} workload, oracle/ CPU restatement (OpenMP, {threads} threads, "
+                      f"reference packed layout), median of {steps} applies after 3 warm-up; "
+                      f"ms/apply {med * 1e3:.2f}"}, z
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="1M+contacts", choices=CONFIG_ORDER)
+    ap.add_argument("--cpu-steps", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    mesh, cfg = meshgen.build_config(args.config)
+    cfg = dict(cfg, name=args.config)
+    contacts = meshgen.vf_contacts(mesh, cfg["contacts"], seed=3) if cfg["contacts"] else None
+    t0 = time.perf_counter()
+    P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts, device=local)
+    setup_s = time.perf_counter() - t0
+    info = P.info()
+    st0 = P.stats()
+    seed = 0x5EED + CONFIG_ORDER.index(args.config)
+    r_np = meshgen.residual(mesh.nV, seed)
+    r = torch.from_numpy(r_np).cuda()
+    z = torch.zeros_like(r)
+    # an explicit stream: torch's default stream handle is 0, which the C ABI
+    # maps to the handle's own stream
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        P.PreconditioningDevice(z, r, sptr)
+    torch.cuda.synchronize()
+
+    # timed region: K applies, bracketed by barrier + synchronize (no
+    # instrumentation inside: per-kernel events cost ~10 us per apply).
+    barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    w0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        P.PreconditioningDevice(z, r, sptr)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    wall = time.perf_counter() - w0
+    elapsed = ev0.elapsed_time(ev1) / 1e3
+
+    # kernel-duration pass: the same K applies with the library's HIP events
+    # recorded on the apply stream around each kernel group (roofline source).
+    P.set_profiling(True)
+    torch.cuda.synchronize()
+    ev2, ev3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev2.record(stream)
+    for _ in range(args.steps):
+        P.PreconditioningDevice(z, r, sptr)
+    ev3.record(stream)
+    torch.cuda.synchronize()
+    elapsed_ev = ev2.elapsed_time(ev3) / 1e3
+    st = P.stats()
+    P.set_profiling(False)
+
+    t_max = elapsed
+    if dist is not None:
+        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+
+    fine_bytes, apply_bytes = algorithmic_bytes(info)
+    fine_s = st["fine_ms_avg"] / 1e3
+    achieved = fine_bytes / fine_s / 1e9 if fine_s > 0 else None
+    value = world * args.steps / t_max
+    ms_per_step = t_max / args.steps * 1e3
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "applies/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": {
+                "10k": "10k-vertex cloth (100x100 grid), 1 level",
+                "256k": "256k-vertex cloth (512x512 grid), 3 levels",
+                "1M+contacts": "1M-vertex cloth (1024x1024 grid) + 100k VF contact stencils, 4 levels",
+                "1M": "1M-vertex cloth (1024x1024 grid), 4 levels",
+                "4M-tet": "4M-vertex tet lattice (160^3, valence 14), 4 levels",
+            }[args.config],
+            "name": args.config,
+            "num_verts": info["num_verts"],
+            "levels": info["num_levels"],
+            "subdomain": 32,
+            "blocks": info["num_blocks"],
+            "fine_blocks": info["num_fine_blocks"],
+            "contact_stencils": info["num_stencils"],
+            "parallelism": "replicas" if world > 1 else "single-gpu",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_solve_fine (fused gather + level-0 block solves + prolongation)",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": None,
+            "bytes_per_launch": fine_bytes,
+            "avg_launch_ms": round(st["fine_ms_avg"], 5),
+        },
+        "apply_breakdown_ms": {
+            "restrict": round(st["restrict_ms_avg"], 5),
+            "coarse_solve": round(st["coarse_ms_avg"], 5),
+            "fine_solve": round(st["fine_ms_avg"], 5),
+            "events_total": round(st["apply_ms_avg"], 5),
+            "ms_per_step_with_kernel_events": round(elapsed_ev / args.steps * 1e3, 5),
+        },
+        "apply_algorithmic_GBps": round(apply_bytes / (t_max / args.steps) / 1e9, 1),
+        "apply_bytes": apply_bytes,
+        "prepare_ms": round(st0["prepare_ms"], 3),
+        "prepare_breakdown_ms": {"levels": round(st0["prepare_levels_ms"], 3),
+                                 "assemble": round(st0["prepare_assemble_ms"], 3),
+                                 "factor": round(st0["prepare_factor_ms"], 3)},
+        "allocate_ms": round(st0["allocate_ms"], 3),
+        "host_setup_s": round(setup_s, 2),
+        "wall_s_timed": round(wall, 4),
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cb, z_cpu = cpu_baseline(mesh, cfg, contacts, r_np, args.cpu_steps)
+            z_gpu = z.cpu().numpy()
+            cb["z_rel_err_vs_gpu"] = float(np.linalg.norm(z_gpu[:, :3] - z_cpu[:, :3]) /
+                                           np.linalg.norm(z_cpu[:, :3]))
+            out["cpu_baseline"] = cb
+        except Exception as e:  # the baseline is reported, never required
+            log(f"cpu_baseline failed: {e!r}")
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

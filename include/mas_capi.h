@@ -78,13 +78,17 @@ typedef struct {
 } mas_info;
 
 typedef struct {
-    /* milliseconds of the most recent call of each phase (device time) */
-    double allocate_ms, prepare_ms, apply_ms;
+    /* device time (ms) of the most recent call of each phase */
+    double allocate_ms, prepare_ms;
     double prepare_levels_ms, prepare_assemble_ms, prepare_factor_ms;
-    /* per-kernel device time of the most recent mas_apply_device with
-     * profiling enabled (mas_set_profiling), milliseconds */
-    double apply_restrict_ms, apply_coarse_ms, apply_fine_ms;
-    int64_t apply_calls;
+    int64_t apply_calls;       /* applies since mas_create */
+    /* averages over the applies recorded while profiling was on (mas_set_profiling),
+       measured with HIP events on the apply stream around each kernel group */
+    int64_t profiled_applies;
+    double apply_ms_avg;       /* first restrict kernel start -> fine kernel end */
+    double restrict_ms_avg;    /* level 0->1 ... L-2->L-1 restriction kernels */
+    double coarse_ms_avg;      /* coarse-level block solves */
+    double fine_ms_avg;        /* fused gather + level-0 block solve + prolongation (dominant kernel) */
 } mas_stats;
 
 /* lifecycle */
@@ -120,7 +124,8 @@ int mas_apply(mas_handle h, float* z4, const float* r4);
  * stream: hipStream_t (NULL = handle stream).  Asynchronous. */
 int mas_apply_device(mas_handle h, float* d_z4, const float* d_r4, void* stream);
 
-/* Record per-kernel HIP events inside mas_apply_device (for mas_stats). */
+/* Record HIP events around the apply kernels of every mas_apply_device call
+ * (up to 4096 applies) and reset the averages in mas_stats. */
 int mas_set_profiling(mas_handle h, int enable);
 
 /* introspection / parity */

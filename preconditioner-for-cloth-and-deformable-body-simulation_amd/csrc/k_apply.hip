@@ -159,55 +159,53 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve_coarse(const float4* __
     if (valid && lane < 32) zc[node] = make_float4(out.x, out.y, out.z, 0.f);
 }
 
-// Segmented sum of a 32-lane bank by parent id, in lane order.  Lane with the
-// lowest index of each parent writes the sum.
-__device__ __forceinline__ void bank_sum_store(float3 val, int p, bool valid, int n, int half, float4* __restrict__ rc,
-                                               int begin1) {
+// Segmented sum of a 32-lane bank by parent id, in lane order from +0 (the
+// reference's owner loop, .cpp:1560-1572): each bank stages (value, parent)
+// in LDS, every lane walks the 32 entries with broadcast ds_read_b128 and adds
+// the ones with its parent; the lowest lane of each parent stores the sum.
+__device__ __forceinline__ void bank_sum_store(float3 val, int p, bool valid, float4* __restrict__ rc, int begin1) {
+    __shared__ float4 buf[kApplyThreads];
+    const int t = threadIdx.x, n = t & 31, base = t & ~31;
+    buf[t] = make_float4(val.x, val.y, val.z, __int_as_float(p));
+    __syncthreads();
     float ax = 0.f, ay = 0.f, az = 0.f;
-    int first = -1;
-#pragma unroll
+    bool leader = true;
+#pragma unroll 8
     for (int j = 0; j < 32; ++j) {
-        const int p0 = __builtin_amdgcn_readlane(p, j), p1 = __builtin_amdgcn_readlane(p, 32 + j);
-        const float x0 = rd_lane(val.x, j), x1 = rd_lane(val.x, 32 + j);
-        const float y0 = rd_lane(val.y, j), y1 = rd_lane(val.y, 32 + j);
-        const float z0 = rd_lane(val.z, j), z1 = rd_lane(val.z, 32 + j);
-        const int pj = half ? p1 : p0;
-        if (pj == p) {
-            ax = __fadd_rn(ax, half ? x1 : x0);
-            ay = __fadd_rn(ay, half ? y1 : y0);
-            az = __fadd_rn(az, half ? z1 : z0);
-            if (first < 0) first = j;
+        const float4 e = buf[base + j];
+        if (__float_as_int(e.w) == p) {
+            ax = __fadd_rn(ax, e.x);
+            ay = __fadd_rn(ay, e.y);
+            az = __fadd_rn(az, e.z);
+            leader = leader && (j >= n);
         }
     }
-    if (valid && first == n) rc[p - begin1] = make_float4(ax, ay, az, 0.f);
+    if (valid && leader) rc[p - begin1] = make_float4(ax, ay, az, 0.f);
 }
 
 __global__ __launch_bounds__(kApplyThreads) void k_restrict_l0(int nV, int nBanks, const float4* __restrict__ r,
                                                               const int4* __restrict__ vmap, float4* __restrict__ rc,
                                                               int begin1) {
-    const int lane = threadIdx.x & 63, n = lane & 31, half = lane & 32;
-    const int bank = (blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6)) * 2 + (half >> 5);
-    const int v = bank * 32 + n;
+    const int bank = blockIdx.x * (kApplyThreads / 32) + (threadIdx.x >> 5);
+    const int v = bank * 32 + (threadIdx.x & 31);
     const bool valid = bank < nBanks && v < nV;
     const int4 m = vmap[valid ? v : 0];
     const float4 rv = r[m.x];
     const float3 val = valid ? make_float3(rv.x, rv.y, rv.z) : make_float3(0.f, 0.f, 0.f);
-    bank_sum_store(val, valid ? m.y : -1, valid, n, half, rc, begin1);
+    bank_sum_store(val, valid ? m.y : -1, valid, rc, begin1);
 }
 
 __global__ __launch_bounds__(kApplyThreads) void k_restrict_lx(int begin, int count, const int* __restrict__ gn,
                                                               float4* __restrict__ rc, int begin1) {
-    const int lane = threadIdx.x & 63, n = lane & 31, half = lane & 32;
-    const int bank = (blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6)) * 2 + (half >> 5);
-    const int local = bank * 32 + n;
+    const int local = blockIdx.x * kApplyThreads + threadIdx.x;
     const bool valid = local < count;
     const int node = begin + (valid ? local : 0);
     const float4 rv = rc[node - begin1];
     const float3 val = valid ? make_float3(rv.x, rv.y, rv.z) : make_float3(0.f, 0.f, 0.f);
-    bank_sum_store(val, valid ? gn[node] : -1, valid, n, half, rc, begin1);
+    bank_sum_store(val, valid ? gn[node] : -1, valid, rc, begin1);
 }
 
-static inline int grid_for_banks(int banks) { return cdiv(banks, 2 * (kApplyThreads / 64)); }
+static inline int grid_for_banks(int banks) { return cdiv(banks, kApplyThreads / 32); }
 static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThreads / 64); }
 
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
@@ -217,24 +215,23 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     const float4* inv = P<float4>(h->inv);
     float4* rc = P<float4>(h->Rc);
     float4* zc = P<float4>(h->Zc);
-    const bool prof = h->profiling;
-    if (prof) hipEventRecord(h->ev[4], s);
+    hipEvent_t* ev = nullptr;
+    if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
+    if (ev) hipEventRecord(ev[0], s);
     if (L > 1) {
         k_restrict_l0<<<grid_for_banks(h->nFineBlk), kApplyThreads, 0, s>>>(nV, h->nFineBlk, d_r, vmap, rc, begin1);
         for (int l = 1; l + 1 < L; ++l) {
             const int cnt = h->levelSize[2 * l], beg = h->levelSize[2 * l + 1];
-            k_restrict_lx<<<grid_for_banks(cdiv(cnt, 32)), kApplyThreads, 0, s>>>(beg, cnt, P<int>(h->goingNext), rc,
+            k_restrict_lx<<<cdiv(cnt, kApplyThreads), kApplyThreads, 0, s>>>(beg, cnt, P<int>(h->goingNext), rc,
                                                                                    begin1);
         }
     }
-    if (prof) hipEventRecord(h->ev[5], s);
-    if (prof) hipEventRecord(h->ev[6], s);
+    if (ev) hipEventRecord(ev[1], s);
     if (L > 1) {
         const int nc = h->nBlk - h->nFineBlk;
         k_solve_coarse<<<grid_for_blocks(nc), kApplyThreads, 0, s>>>(inv, h->nFineBlk, nc, rc, begin1, zc);
     }
-    if (prof) hipEventRecord(h->ev[7], s);
-    if (prof) hipEventRecord(h->ev[8], s);
+    if (ev) hipEventRecord(ev[2], s);
     const int g = grid_for_blocks(h->nFineBlk);
     switch (L < 4 ? L - 1 : 3) {
         case 0: k_solve_fine<0><<<g, kApplyThreads, 0, s>>>(inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z); break;
@@ -242,7 +239,7 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
         case 2: k_solve_fine<2><<<g, kApplyThreads, 0, s>>>(inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z); break;
         default: k_solve_fine<3><<<g, kApplyThreads, 0, s>>>(inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z); break;
     }
-    if (prof) hipEventRecord(h->ev[9], s);
+    if (ev) hipEventRecord(ev[3], s);
     h->stats.apply_calls++;
     return hip_check(h, hipGetLastError(), "apply kernels");
 }

@@ -6,6 +6,7 @@
 // (SeSchwarzPreconditioner.h:56-63).
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <new>
 
 #include "mas_internal.h"
@@ -103,6 +104,7 @@ int mas_destroy(mas_handle h) {
     h->for_each_buffer([](Buffer& b) { release(b); });
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
+    for (auto& e : h->prof) hipEventDestroy(e);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return MAS_OK;
@@ -186,7 +188,17 @@ int mas_apply(mas_handle h, float* z4, const float* r4) {
 
 int mas_set_profiling(mas_handle h, int enable) {
     if (!h) return MAS_ERR_ARG;
+    hipSetDevice(h->device);
+    if (enable && h->prof.empty()) {
+        h->prof.resize(4 * kProfRing);
+        for (auto& e : h->prof)
+            if (hipEventCreate(&e) != hipSuccess) return fail(h, MAS_ERR_HIP, "hipEventCreate");
+    }
+    if (h->stream) hipStreamSynchronize(h->stream);
     h->profiling = enable != 0;
+    h->profRecorded = 0;
+    h->stats.profiled_applies = 0;
+    h->stats.apply_ms_avg = h->stats.restrict_ms_avg = h->stats.coarse_ms_avg = h->stats.fine_ms_avg = 0.0;
     return MAS_OK;
 }
 
@@ -211,13 +223,25 @@ int mas_get_info(mas_handle h, mas_info* out) {
 
 int mas_get_stats(mas_handle h, mas_stats* out) {
     if (!h || !out) return MAS_ERR_ARG;
-    if (h->profiling && h->stats.apply_calls > 0) {
-        hipEventSynchronize(h->ev[9]);
-        float t = 0.f;
-        if (hipEventElapsedTime(&t, h->ev[4], h->ev[5]) == hipSuccess) h->stats.apply_restrict_ms = t;
-        if (hipEventElapsedTime(&t, h->ev[6], h->ev[7]) == hipSuccess) h->stats.apply_coarse_ms = t;
-        if (hipEventElapsedTime(&t, h->ev[8], h->ev[9]) == hipSuccess) h->stats.apply_fine_ms = t;
-        if (hipEventElapsedTime(&t, h->ev[4], h->ev[9]) == hipSuccess) h->stats.apply_ms = t;
+    const int n = std::min(h->profRecorded, kProfRing);
+    if (n > 0) {
+        hipSetDevice(h->device);
+        double sa = 0, sr = 0, sc = 0, sf = 0;
+        for (int i = 0; i < n; ++i) {
+            hipEvent_t* e = &h->prof[4 * i];
+            if (hipEventSynchronize(e[3]) != hipSuccess) return fail(h, MAS_ERR_HIP, "profiling event sync");
+            float a = 0, r = 0, c = 0, f = 0;
+            hipEventElapsedTime(&a, e[0], e[3]);
+            hipEventElapsedTime(&r, e[0], e[1]);
+            hipEventElapsedTime(&c, e[1], e[2]);
+            hipEventElapsedTime(&f, e[2], e[3]);
+            sa += a; sr += r; sc += c; sf += f;
+        }
+        h->stats.profiled_applies = n;
+        h->stats.apply_ms_avg = sa / n;
+        h->stats.restrict_ms_avg = sr / n;
+        h->stats.coarse_ms_avg = sc / n;
+        h->stats.fine_ms_avg = sf / n;
     }
     *out = h->stats;
     return MAS_OK;

@@ -17,6 +17,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/mas_capi.h"
 
@@ -27,6 +28,7 @@ constexpr int kBlockFloats = 4656;      // (96*97)/2 packed symmetric 96x96
 constexpr int kBlockF4 = kBlockFloats / 4;  // 1164 float4 per block
 constexpr int kMaxLevels = 5;             // reference B-6
 constexpr int kDenseFloats = 96 * 96;
+constexpr int kProfRing = 4096;          // applies recorded while profiling
 
 // Stencil, SeCollisionElements.h:60-69 (device copy; direction xyz only).
 struct DevStencil {
@@ -75,8 +77,11 @@ struct mas_context {
     mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
     // hipcub scratch
     mas::Buffer cubTemp;
-    // events: [0..1] allocate, [2..3] prepare, [4..9] apply kernels
-    hipEvent_t ev[12] = {};
+    // events: [0..1] allocate, [2..3] prepare
+    hipEvent_t ev[4] = {};
+    // profiling ring: 4 events per apply (start, restrict end, coarse end, fine end)
+    std::vector<hipEvent_t> prof;
+    int profRecorded = 0;
     mas_stats stats{};
 
     template <class F>

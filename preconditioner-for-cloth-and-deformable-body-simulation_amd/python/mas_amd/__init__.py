@@ -48,9 +48,10 @@ class mas_info(ctypes.Structure):
 
 
 class mas_stats(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_double) for n in ("allocate_ms", "prepare_ms", "apply_ms", "prepare_levels_ms",
-                                               "prepare_assemble_ms", "prepare_factor_ms", "apply_restrict_ms",
-                                               "apply_coarse_ms", "apply_fine_ms")] + [("apply_calls", ctypes.c_int64)]
+    _fields_ = [(n, ctypes.c_double) for n in ("allocate_ms", "prepare_ms", "prepare_levels_ms",
+                                               "prepare_assemble_ms", "prepare_factor_ms")] + \
+               [("apply_calls", ctypes.c_int64), ("profiled_applies", ctypes.c_int64)] + \
+               [(n, ctypes.c_double) for n in ("apply_ms_avg", "restrict_ms_avg", "coarse_ms_avg", "fine_ms_avg")]
 
 
 class MasError(RuntimeError):

@@ -98,7 +98,8 @@ def test_device_path_and_determinism():
     z_host = P.Preconditioning(None, r)
     rd = torch.from_numpy(r).cuda()
     zd = torch.zeros_like(rd)
-    s = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
     P.PreconditioningDevice(zd, rd, s.cuda_stream)
     s.synchronize()
     z1 = zd.cpu().numpy().copy()
