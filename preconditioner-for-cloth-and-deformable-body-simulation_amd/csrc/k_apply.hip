@@ -1,35 +1,36 @@
 // k_apply.hip -- Preconditioning (.cpp:100-110, 1548-1719): the hot path.
 //
-//   k_restrict_l0   R1 = level-1 sums of r gathered through the Morton map
-//                   (BuildResidualHierarchy .cpp:1558-1574); sums run in lane
-//                   order from +0, exactly as the reference's owner loop.
-//   k_restrict_lx   R_{l+1} from R_l for l >= 1 (deterministic per-bank sums;
-//                   .cpp:1577-1591 sums level-1 values straight into every
-//                   ancestor -- same value up to fp association).
-//   k_solve<COARSE> Z_b = Inv_b R_b for every coarse block (SchwarzLocalXSym
-//                   .cpp:1600-1696).
-//   k_solve<FINE>   the same for every level-0 block, fused with the gather
-//                   r[s2o[v]] and the prolongation
-//                   z[s2o[v]] = Z0 + Z1[a1] + Z2[a2] + Z3[a3] (CollectFinalZ
-//                   .cpp:1698-1719, min(L,4)-1 coarse levels, B-6).
+// Per apply, L launches on one stream:
+//   k_coarse<level 1>   per level-1 block (one wave): R1 of its 32 nodes from
+//                       r gathered through the Morton map, summed per parent
+//                       in lane order from +0 exactly as the reference's owner
+//                       loop (BuildResidualHierarchy .cpp:1558-1574); then
+//                       Z1 = Inv_b R1 (SchwarzLocalXSym .cpp:1600-1696).
+//   k_coarse<level l>   l = 2..L-1: R_l from R_{l-1} the same way (level 2 is
+//                       the reference's level-1-id-order sum, .cpp:1581-1590;
+//                       level >= 3 sums R_{l-1}, same value up to fp
+//                       association), then Z_l.
+//   k_solve_fine        every level-0 block fused with the gather r[s2o[v]]
+//                       and the prolongation z[s2o[v]] = Z0 + Z1[a1] + Z2[a2]
+//                       + Z3[a3] (CollectFinalZ .cpp:1698-1719, min(L,4)-1
+//                       coarse levels, B-6).  This kernel streams 18 624 B of
+//                       packed inverse per block and dominates the apply.
 //
-// Block solve mapping (layout.h): a wave64 solves two blocks, one per 32-lane
-// half; lane n owns node n.  The 18 624-byte packed inverse is streamed by 36
-// float4 loads + one 12-byte tail load per lane (2 x 512 contiguous bytes per
-// wave-instruction) straight into registers; the symmetric mat-vec then needs
-// only ds_bpermute rotations: for s = 1..15 lane n multiplies G(n, n+s) with
-// r_{n+s} and sends G^T r_n to lane n+s.  No LDS, no atomics, no barriers.
-// The kernel is bound by HBM bandwidth (~1 flop/byte).
+// Block solve (layout.h): one wave64 per 32-node block, lane 32h + n owns
+// node n; the halves split the 3x3 node-pair blocks by rotation distance.
+// The packed inverse arrives through 18 float4 loads per lane (1 KiB
+// contiguous per wave-instruction) plus a 12-byte tail straight into
+// registers; the symmetric mat-vec is 8 rotation steps of ds_bpermute
+// shuffles (lane n multiplies G(n, n+s) with r_{n+s} and returns G^T r_n to
+// lane n+s) and one cross-half add.  No LDS, no atomics, no barriers.
+#include <vector>
+
 #include "layout.h"
 #include "mas_internal.h"
 
 namespace mas {
 
 constexpr int kApplyThreads = 256;  // 4 waves = 4 blocks per workgroup
-
-__device__ __forceinline__ float rd_lane(float x, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
-}
 
 // One rotation step: out += G r_src, and lane dst receives G^T r_own.
 __device__ __forceinline__ void pair_step(float3& out, const float (&G)[9], float3 r, int src, int dst) {
@@ -91,12 +92,15 @@ __device__ __forceinline__ float3 block_solve(const float (&g)[kRecord], const f
     return out;
 }
 
+template <bool NT = false>
 __device__ __forceinline__ void load_record(const float4* __restrict__ inv, int blk, int lane, float (&g)[kRecord],
                                             float (&tl)[3]) {
     const float4* b = inv + (size_t)blk * kBlockF4 + lane;
 #pragma unroll
     for (int q = 0; q < kRecord / 4; ++q) {
-        const float4 x = b[q * 64];
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f* bp = reinterpret_cast<const v4f*>(b + q * 64);
+        const v4f x = NT ? __builtin_nontemporal_load(bp) : *bp;
         g[4 * q + 0] = x.x;
         g[4 * q + 1] = x.y;
         g[4 * q + 2] = x.z;
@@ -110,12 +114,14 @@ __device__ __forceinline__ void load_record(const float4* __restrict__ inv, int 
 }
 
 // Fine blocks: gather r through the Morton map, solve, prolongate, scatter z.
-template <int NPROL>
-__global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __restrict__ inv, int nFineBlk, int nV,
-                                                             const float4* __restrict__ r,
-                                                             const int4* __restrict__ vmap,
-                                                             const float4* __restrict__ zc, int begin1,
-                                                             float4* __restrict__ z) {
+// The packed inverses are read exactly once per apply (630 MB at 1M, more
+// than the 256 MiB Infinity Cache), so they are loaded nontemporal: measured
+// 98.8 vs 109.7 us per launch at 1M against default-policy loads (VAR = 0,
+// env MAS_FINE_VARIANT=0 keeps that variant for A/B runs).
+template <int NPROL, int VAR>
+__device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, int nFineBlk, int nV,
+                                                const float4* __restrict__ r, const int4* __restrict__ vmap,
+                                                const float4* __restrict__ zc, int begin1, float4* __restrict__ z) {
     const int lane = threadIdx.x & 63, n = lane & 31;
     const int blk = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
     const bool bvalid = blk < nFineBlk;
@@ -123,7 +129,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __re
     const bool vvalid = bvalid && v < nV;
     const int4 m = vmap[vvalid ? v : 0];
     float g[kRecord], tl[3];
-    load_record(inv, bvalid ? blk : 0, lane, g, tl);
+    load_record<VAR == 1>(inv, bvalid ? blk : 0, lane, g, tl);
     const float4 rv = r[m.x];
     const float3 rr = vvalid ? make_float3(rv.x, rv.y, rv.z) : make_float3(0.f, 0.f, 0.f);
     float3 out = block_solve(g, tl, rr, lane);
@@ -143,153 +149,165 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __re
     z[m.x] = make_float4(out.x, out.y, out.z, 0.f);
 }
 
-// Coarse blocks [blk0, blk0 + nb): Zc = Inv Rc (node-indexed from begin1).
-__global__ __launch_bounds__(kApplyThreads) void k_solve_coarse(const float4* __restrict__ inv, int blk0, int nb,
-                                                               const float4* __restrict__ rc, int begin1,
-                                                               float4* __restrict__ zc) {
-    const int lane = threadIdx.x & 63, n = lane & 31;
-    const int rel = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
-    const bool valid = rel < nb;
-    const int blk = blk0 + (valid ? rel : 0);
-    const int node = blk * 32 + n - begin1;
-    float g[kRecord], tl[3];
-    load_record(inv, blk, lane, g, tl);
-    const float4 rv = rc[node];
-    const float3 out = block_solve(g, tl, make_float3(rv.x, rv.y, rv.z), lane);
-    if (valid && lane < 32) zc[node] = make_float4(out.x, out.y, out.z, 0.f);
+
+template <int NPROL, int VAR>
+__global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __restrict__ inv, int nFineBlk, int nV,
+                                                             const float4* __restrict__ r,
+                                                             const int4* __restrict__ vmap,
+                                                             const float4* __restrict__ zc, int begin1,
+                                                             float4* __restrict__ z) {
+    solve_fine_body<NPROL, VAR>(inv, nFineBlk, nV, r, vmap, zc, begin1, z);
 }
 
-// Segmented sum of a 32-lane bank by parent id, in lane order from +0 (the
-// reference's owner loop, .cpp:1560-1572): each bank stages (value, parent)
-// in LDS, every lane walks the 32 entries with broadcast ds_read_b128 and adds
-// the ones with its parent; the lowest lane of each parent stores the sum.
-__device__ __forceinline__ void bank_sum_store(float3 val, int p, bool valid, float4* __restrict__ rc, int begin1) {
-    __shared__ float4 buf[kApplyThreads];
-    const int t = threadIdx.x, n = t & 31, base = t & ~31;
-    buf[t] = make_float4(val.x, val.y, val.z, __int_as_float(p));
-    __syncthreads();
-    float ax = 0.f, ay = 0.f, az = 0.f;
-    bool leader = true;
-#pragma unroll 8
+// One coarse level l >= 1, one wave per 32-node block; lane n (half 0) owns
+// node P = 32 blk + n.  members[P] = (child bank, component mask): the
+// children of P are exactly the lanes of that mask (they are the connected
+// component the clustering merged into P, .cpp:590-625 / 917-954).  Every
+// child value is gathered up front (one latency), then lane n adds its
+// children in lane order from +0 -- the reference's accumulation order for
+// level 1 (.cpp:1560-1572) and level 2 (level-1 id order, .cpp:1581-1590);
+// level >= 3 sums R_{l-1} (the reference sums R_1 directly: same value up
+// to fp association).  Then Z_l = Inv_b R_l; R_l and Z_l are stored.
+template <bool FROM_VERTS>
+__global__ __launch_bounds__(kApplyThreads) void k_coarse(const float4* __restrict__ inv, int blkBegin, int nb,
+                                                         int count, const int2* __restrict__ members,
+                                                         int childBegin, const int* __restrict__ s2o,
+                                                         const float4* __restrict__ r, float4* __restrict__ rc,
+                                                         float4* __restrict__ zc, int begin1) {
+    const int lane = threadIdx.x & 63, n = lane & 31;
+    const int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
+    if (w >= nb) return;  // wave-uniform
+    const int blk = blkBegin + w;
+    const int node = blk * 32 + n;
+    float g[kRecord], tl[3];
+    load_record<true>(inv, blk, lane, g, tl);
+    const bool own = lane < 32 && (node - blkBegin * 32) < count;
+    const int2 mb = own ? members[node - begin1] : make_int2(0, 0);
+    const unsigned msk = (unsigned)mb.y;
+    const int base = mb.x * 32;
+    int src[32];
+    if (FROM_VERTS) {  // the bank's 32 Morton->original ids: 8 x 16-byte loads
+        const int4* s4 = reinterpret_cast<const int4*>(s2o + base);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int4 t = s4[q];
+            src[4 * q + 0] = t.x;
+            src[4 * q + 1] = t.y;
+            src[4 * q + 2] = t.z;
+            src[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) src[j] = childBegin + base + j - begin1;
+    }
+    float vx[32], vy[32], vz[32];
+#pragma unroll
     for (int j = 0; j < 32; ++j) {
-        const float4 e = buf[base + j];
-        if (__float_as_int(e.w) == p) {
-            ax = __fadd_rn(ax, e.x);
-            ay = __fadd_rn(ay, e.y);
-            az = __fadd_rn(az, e.z);
-            leader = leader && (j >= n);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((msk >> j) & 1u) v = FROM_VERTS ? r[src[j]] : rc[src[j]];
+        vx[j] = v.x;
+        vy[j] = v.y;
+        vz[j] = v.z;
+    }
+    float ax = 0.f, ay = 0.f, az = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        if ((msk >> j) & 1u) {
+            ax = __fadd_rn(ax, vx[j]);
+            ay = __fadd_rn(ay, vy[j]);
+            az = __fadd_rn(az, vz[j]);
         }
     }
-    if (valid && leader) rc[p - begin1] = make_float4(ax, ay, az, 0.f);
+    // half 1 takes node n's residual from lane n
+    ax = __shfl(ax, n);
+    ay = __shfl(ay, n);
+    az = __shfl(az, n);
+    const float3 out = block_solve(g, tl, make_float3(ax, ay, az), lane);
+    if (lane < 32) {
+        rc[node - begin1] = make_float4(ax, ay, az, 0.f);
+        zc[node - begin1] = make_float4(out.x, out.y, out.z, 0.f);
+    }
 }
 
-__global__ __launch_bounds__(kApplyThreads) void k_restrict_l0(int nV, int nBanks, const float4* __restrict__ r,
-                                                              const int4* __restrict__ vmap, float4* __restrict__ rc,
-                                                              int begin1) {
-    const int bank = blockIdx.x * (kApplyThreads / 32) + (threadIdx.x >> 5);
-    const int v = bank * 32 + (threadIdx.x & 31);
-    const bool valid = bank < nBanks && v < nV;
-    const int4 m = vmap[valid ? v : 0];
-    const float4 rv = r[m.x];
-    const float3 val = valid ? make_float3(rv.x, rv.y, rv.z) : make_float3(0.f, 0.f, 0.f);
-    bank_sum_store(val, valid ? m.y : -1, valid, rc, begin1);
+// Prepare-time: members[P] = (bank, closure mask) of the component that
+// became coarse node P; written by the component's lowest lane.
+__global__ __launch_bounds__(256) void k_members(int nChild, int childBegin, const unsigned* __restrict__ masks,
+                                                 const int* __restrict__ gn, int begin1, int2* __restrict__ members) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nChild) return;
+    const unsigned m = masks[c];
+    const unsigned lane = c & 31;
+    if (__popc(m & ((1u << lane) - 1u)) != 0) return;
+    members[gn[childBegin + c] - begin1] = make_int2(c >> 5, (int)m);
 }
 
-__global__ __launch_bounds__(kApplyThreads) void k_restrict_lx(int begin, int count, const int* __restrict__ gn,
-                                                              float4* __restrict__ rc, int begin1) {
-    const int local = blockIdx.x * kApplyThreads + threadIdx.x;
-    const bool valid = local < count;
-    const int node = begin + (valid ? local : 0);
-    const float4 rv = rc[node - begin1];
-    const float3 val = valid ? make_float3(rv.x, rv.y, rv.z) : make_float3(0.f, 0.f, 0.f);
-    bank_sum_store(val, valid ? gn[node] : -1, valid, rc, begin1);
-}
-
-static inline int grid_for_banks(int banks) { return cdiv(banks, kApplyThreads / 32); }
 static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThreads / 64); }
+
+template <int NPROL>
+static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int nFine, int nV, const float4* r,
+                          const int4* vmap, const float4* zc, int begin1, float4* z) {
+    if (var == 0) k_solve_fine<NPROL, 0><<<g, kApplyThreads, 0, s>>>(inv, nFine, nV, r, vmap, zc, begin1, z);
+    else k_solve_fine<NPROL, 1><<<g, kApplyThreads, 0, s>>>(inv, nFine, nV, r, vmap, zc, begin1, z);
+}
+
+static void launch_fine(int nprol, int var, int g, hipStream_t s, const float4* inv, int nFine, int nV,
+                        const float4* r, const int4* vmap, const float4* zc, int begin1, float4* z) {
+    switch (nprol) {
+        case 0: launch_fine_n<0>(var, g, s, inv, nFine, nV, r, vmap, zc, begin1, z); break;
+        case 1: launch_fine_n<1>(var, g, s, inv, nFine, nV, r, vmap, zc, begin1, z); break;
+        case 2: launch_fine_n<2>(var, g, s, inv, nFine, nV, r, vmap, zc, begin1, z); break;
+        default: launch_fine_n<3>(var, g, s, inv, nFine, nV, r, vmap, zc, begin1, z); break;
+    }
+}
 
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     const int L = h->L, nV = h->nV;
     const int begin1 = h->levelSize[3];
-    const int4* vmap = P<int4>(h->vmap);
     const float4* inv = P<float4>(h->inv);
     float4* rc = P<float4>(h->Rc);
     float4* zc = P<float4>(h->Zc);
     hipEvent_t* ev = nullptr;
     if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
     if (ev) hipEventRecord(ev[0], s);
-    if (L > 1) {
-        k_restrict_l0<<<grid_for_banks(h->nFineBlk), kApplyThreads, 0, s>>>(nV, h->nFineBlk, d_r, vmap, rc, begin1);
-        for (int l = 1; l + 1 < L; ++l) {
-            const int cnt = h->levelSize[2 * l], beg = h->levelSize[2 * l + 1];
-            k_restrict_lx<<<cdiv(cnt, kApplyThreads), kApplyThreads, 0, s>>>(beg, cnt, P<int>(h->goingNext), rc,
-                                                                                   begin1);
-        }
+    for (int l = 1; l < L; ++l) {
+        const int cnt = h->levelSize[2 * l], beg = h->levelSize[2 * l + 1];
+        const int nb = ceil32(cnt) / 32;
+        if (l == 1)
+            k_coarse<true><<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int2>(h->members), 0,
+                                                                          P<int>(h->s2o), d_r, rc, zc, begin1);
+        else
+            k_coarse<false><<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int2>(h->members),
+                                                                           h->levelSize[2 * (l - 1) + 1], nullptr,
+                                                                           nullptr, rc, zc, begin1);
+        if (ev && l == 1) hipEventRecord(ev[1], s);
     }
-    if (ev) hipEventRecord(ev[1], s);
-    if (L > 1) {
-        const int nc = h->nBlk - h->nFineBlk;
-        k_solve_coarse<<<grid_for_blocks(nc), kApplyThreads, 0, s>>>(inv, h->nFineBlk, nc, rc, begin1, zc);
-    }
+    if (ev && L == 1) hipEventRecord(ev[1], s);
     if (ev) hipEventRecord(ev[2], s);
+    const int4* vmap = P<int4>(h->vmap);
     const int g = grid_for_blocks(h->nFineBlk);
-    switch (L < 4 ? L - 1 : 3) {
-        case 0: k_solve_fine<0><<<g, kApplyThreads, 0, s>>>(inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z); break;
-        case 1: k_solve_fine<1><<<g, kApplyThreads, 0, s>>>(inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z); break;
-        case 2: k_solve_fine<2><<<g, kApplyThreads, 0, s>>>(inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z); break;
-        default: k_solve_fine<3><<<g, kApplyThreads, 0, s>>>(inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z); break;
-    }
+    launch_fine(L < 4 ? L - 1 : 3, h->fineVariant, g, s, inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z);
     if (ev) hipEventRecord(ev[3], s);
     h->stats.apply_calls++;
     return hip_check(h, hipGetLastError(), "apply kernels");
 }
 
-// ---------------------------------------------------------------------------
-// Prepare orchestration: stencils -> levels -> assembly -> factor
-// ---------------------------------------------------------------------------
-
-int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, const void* ef,
-                const void* ee, const void* vf, const unsigned* efC, const unsigned* eeC, const unsigned* vfC,
-                hipStream_t s) {
+// Apply-side tables, built once per Prepare: members[] for every coarse node.
+int prepare_apply_tables(mas_context* h, hipStream_t s) {
+    const int nV = h->nV, L = h->L;
+    const int begin1 = h->levelSize[3];
+    const int nCoarse = h->totalClusters - begin1;
     int rc;
-    h->prepared = false;
-    hipEventRecord(h->ev[2], s);
-    // .cpp:74-75: fresh copies of the ELL neighbour table
-    if ((rc = hip_check(h, hipMemcpyAsync(h->nbrRem.p, h->nbr.p, (size_t)h->maxNbr * h->nV * 4, hipMemcpyDeviceToDevice, s),
-                        "copy nbr")) ||
-        (rc = hip_check(h, hipMemcpyAsync(h->nbrNumRem.p, h->nbrNum.p, (size_t)h->nV * 4, hipMemcpyDeviceToDevice, s),
-                        "copy nbrNum")))
+    if ((rc = ensure(h, h->members, (size_t)(nCoarse > 0 ? nCoarse : 1) * 8))) return rc;
+    if ((rc = hip_check(h, hipMemsetAsync(h->members.p, 0, (size_t)(nCoarse > 0 ? nCoarse : 1) * 8, s), "memset")))
         return rc;
-    if ((rc = build_stencils(h, ef, ee, vf, efC, eeC, vfC, s))) return rc;
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    if ((rc = run_levels(h, s))) return rc;
-    hipEventRecord(e0, s);
-    if ((rc = run_assemble(h, d_diag9, d_off9, d_ranges, s))) return rc;
-    hipEventRecord(e1, s);
-    if ((rc = run_factor(h, s))) return rc;
-    const int nCoarseNodes = h->totalClusters - h->levelSize[3];
-    if ((rc = ensure(h, h->Rc, (size_t)(nCoarseNodes > 0 ? nCoarseNodes : 1) * 16)) ||
-        (rc = ensure(h, h->Zc, (size_t)(nCoarseNodes > 0 ? nCoarseNodes : 1) * 16)))
-        return rc;
-    if (nCoarseNodes > 0 && (rc = hip_check(h, hipMemsetAsync(h->Rc.p, 0, (size_t)nCoarseNodes * 16, s), "memset Rc")))
-        return rc;
-    hipEventRecord(h->ev[3], s);
-    if ((rc = hip_check(h, hipStreamSynchronize(s), "prepare sync"))) return rc;
-    float a = 0, b = 0, c = 0, t = 0;
-    hipEventElapsedTime(&t, h->ev[2], h->ev[3]);
-    hipEventElapsedTime(&a, h->ev[2], e0);
-    hipEventElapsedTime(&b, e0, e1);
-    hipEventElapsedTime(&c, e1, h->ev[3]);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    h->stats.prepare_ms = t;
-    h->stats.prepare_levels_ms = a;
-    h->stats.prepare_assemble_ms = b;
-    h->stats.prepare_factor_ms = c;
-    h->prepared = true;
-    return MAS_OK;
+    const int* gn = P<int>(h->goingNext);
+    for (int l = 1; l < L; ++l) {
+        const int nChild = l == 1 ? nV : h->levelSize[2 * (l - 1)];
+        const int childBegin = l == 1 ? 0 : h->levelSize[2 * (l - 1) + 1];
+        const unsigned* masks = l == 1 ? P<unsigned>(h->fineMask) : P<unsigned>(h->coarseMask) + (childBegin - begin1);
+        k_members<<<cdiv(nChild, 256), 256, 0, s>>>(nChild, childBegin, masks, gn, begin1, P<int2>(h->members));
+    }
+    return hip_check(h, hipGetLastError(), "apply tables");
 }
 
 }  // namespace mas

@@ -308,7 +308,8 @@ int run_levels(mas_context* h, hipStream_t s) {
         (rc = ensure(h, h->bankCount, (size_t)(nB0 + 1) * 4)) || (rc = ensure(h, h->bankPrefix, (size_t)(nB0 + 1) * 4)) ||
         (rc = ensure(h, h->levelTotal, 16 * 4)) || (rc = ensure(h, h->cst, (size_t)L * nV * 4)) ||
         (rc = ensure(h, h->goingNext, (size_t)(L + 1) * nv32 * 4)) || (rc = ensure(h, h->vmap, (size_t)nV * 16)) ||
-        (rc = ensure(h, h->coarseTables, (size_t)nV * 16)))
+        (rc = ensure(h, h->coarseTables, (size_t)nV * 16)) ||
+        (rc = ensure(h, h->coarseMask, (size_t)L * nv32 * 4)))
         return rc;
     std::fill(h->levelSize, h->levelSize + 18, 0);
     int* cst = P<int>(h->cst);
@@ -341,6 +342,12 @@ int run_levels(mas_context* h, hipStream_t s) {
         k_connect_lx<<<g, 256, 0, s>>>(nV, prev, P<int>(h->nbrNumRem), P<int>(h->nbrRem), next);
         if (h->nStencil) k_collision_connect<<<cdiv(h->nStencil, 256), 256, 0, s>>>(st, h->nStencil, prev, next);
         k_bank_closure<<<cdiv(n, 256), 256, 0, s>>>(n, next, cnt);
+        // keep the level-l component masks (the apply's child lists) before
+        // k_assign_ids overwrites them with ids
+        if (level + 1 < L &&
+            (rc = hip_check(h, hipMemcpyAsync(P<unsigned>(h->coarseMask) + (begin - nv32), next, (size_t)n * 4,
+                                              hipMemcpyDeviceToDevice, s), "save masks")))
+            return rc;
         if ((rc = scan_counts(h, cnt, pre, nb, s))) return rc;
         k_assign_ids<<<cdiv(n, 256), 256, 0, s>>>(n, level, begin, nv32, next, pre, cnt, nb, nullptr, gn, tot);
         k_next_level<<<g, 256, 0, s>>>(nV, prev, next, cst + (size_t)level * nV);

@@ -5,6 +5,7 @@
 // PCG loop that calls the reference's three methods keeps working unchanged
 // (SeSchwarzPreconditioner.h:56-63).
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <new>
@@ -88,6 +89,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
         return MAS_ERR_HIP;
     }
     for (auto& e : h->ev) hipEventCreate(&e);
+    if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
     int rc = upload_slot_table(h);
     if (rc != MAS_OK) {
         mas_destroy(h);

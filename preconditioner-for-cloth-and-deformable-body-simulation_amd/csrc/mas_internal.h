@@ -9,7 +9,7 @@
 //     id and the global ids of the level-1..3 ancestors -- everything the fine
 //     apply kernel needs about a vertex in one 16-byte load.
 //   * inv: per block 4656 fp32 (18 624 B, the reference's packed size) in the
-//     node-pair-rotation layout described in k_apply.hip.
+//     node-pair-rotation layout described in layout.h.
 //   * Rc / Zc: coarse residual / solution, float4 per node id >= begin_1.
 #pragma once
 
@@ -57,6 +57,7 @@ struct mas_context {
     int natL = 0, L = 0, maxNbr = 0;
     int allocCalls = 0;   // reference m_frameIndex semantics (B-1)
     bool allocated = false, prepared = false, profiling = false;
+    int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     int levelSize[2 * 9] = {};
 
@@ -72,7 +73,7 @@ struct mas_context {
     mas::Buffer dense, inv, slotTable;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab;
-    mas::Buffer Rc, Zc;
+    mas::Buffer Rc, Zc, members, coarseMask;
     // staging for host-pointer entry points
     mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
     // hipcub scratch
@@ -91,7 +92,7 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &Rc, &Zc, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &Rc, &Zc, &members, &coarseMask, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }

@@ -1,0 +1,54 @@
+// prepare.hip -- PreparePreconditioner orchestration (.cpp:67-98):
+// stencils -> aggregation levels -> block assembly -> batched factor -> apply tables.
+#include "mas_internal.h"
+
+namespace mas {
+
+int prepare_apply_tables(mas_context* h, hipStream_t s);
+
+int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, const void* ef,
+                const void* ee, const void* vf, const unsigned* efC, const unsigned* eeC, const unsigned* vfC,
+                hipStream_t s) {
+    int rc;
+    h->prepared = false;
+    hipEventRecord(h->ev[2], s);
+    // .cpp:74-75: fresh copies of the ELL neighbour table
+    if ((rc = hip_check(h, hipMemcpyAsync(h->nbrRem.p, h->nbr.p, (size_t)h->maxNbr * h->nV * 4, hipMemcpyDeviceToDevice, s),
+                        "copy nbr")) ||
+        (rc = hip_check(h, hipMemcpyAsync(h->nbrNumRem.p, h->nbrNum.p, (size_t)h->nV * 4, hipMemcpyDeviceToDevice, s),
+                        "copy nbrNum")))
+        return rc;
+    if ((rc = build_stencils(h, ef, ee, vf, efC, eeC, vfC, s))) return rc;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    if ((rc = run_levels(h, s))) return rc;
+    hipEventRecord(e0, s);
+    if ((rc = run_assemble(h, d_diag9, d_off9, d_ranges, s))) return rc;
+    hipEventRecord(e1, s);
+    if ((rc = run_factor(h, s))) return rc;
+    const int nCoarseNodes = h->totalClusters - h->levelSize[3];
+    if ((rc = ensure(h, h->Rc, (size_t)(nCoarseNodes > 0 ? nCoarseNodes : 1) * 16)) ||
+        (rc = ensure(h, h->Zc, (size_t)(nCoarseNodes > 0 ? nCoarseNodes : 1) * 16)))
+        return rc;
+    if (nCoarseNodes > 0 && (rc = hip_check(h, hipMemsetAsync(h->Rc.p, 0, (size_t)nCoarseNodes * 16, s), "memset Rc")))
+        return rc;
+    if ((rc = prepare_apply_tables(h, s))) return rc;
+    hipEventRecord(h->ev[3], s);
+    if ((rc = hip_check(h, hipStreamSynchronize(s), "prepare sync"))) return rc;
+    float a = 0, b = 0, c = 0, t = 0;
+    hipEventElapsedTime(&t, h->ev[2], h->ev[3]);
+    hipEventElapsedTime(&a, h->ev[2], e0);
+    hipEventElapsedTime(&b, e0, e1);
+    hipEventElapsedTime(&c, e1, h->ev[3]);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    h->stats.prepare_ms = t;
+    h->stats.prepare_levels_ms = a;
+    h->stats.prepare_assemble_ms = b;
+    h->stats.prepare_factor_ms = c;
+    h->prepared = true;
+    return MAS_OK;
+}
+
+}  // namespace mas

@@ -129,9 +129,12 @@ class SeSchwarzPreconditioner:
         self._keep = ()
 
     def __del__(self):
-        if getattr(self, "h", None) and self.h.value:
-            self._L.mas_destroy(self.h)
-            self.h = ctypes.c_void_p()
+        try:
+            if getattr(self, "h", None) is not None and self.h.value:
+                self._L.mas_destroy(self.h)
+                self.h.value = None
+        except Exception:  # interpreter shutdown
+            pass
 
     def _check(self, rc, what):
         if rc != MAS_OK:

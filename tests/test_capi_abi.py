@@ -1,0 +1,63 @@
+"""The drop-in boundary without a GPU: libraries load, every declared entry
+point is exported, the facade header keeps the reference's layouts, and the
+library fails loudly (no CPU fallback) when no device is present."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import PKG, REPO
+
+INC = os.path.join(REPO, "include")
+
+
+def _declared(header):
+    src = open(os.path.join(INC, header)).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(mas_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declarations_match_binding_list():
+    import mas_amd
+    assert _declared("mas_capi.h") == sorted(mas_amd.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    import mas_amd
+    lib = ctypes.CDLL(mas_amd.LIB_PATH)
+    missing = [s for s in _declared("mas_capi.h") if not hasattr(lib, s)]
+    assert not missing, missing
+    assert lib.mas_version() == 1
+
+
+def test_facade_exports_reference_methods():
+    import mas_amd
+    out = subprocess.run(["nm", "-D", "-C", "--defined-only", mas_amd.FACADE_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    for sym in ("SE::SeSchwarzPreconditioner::AllocatePrecoditioner(int, int, int)",
+                "SE::SeSchwarzPreconditioner::Preconditioning(SE::SeVec3fSimd*, SE::SeVec3fSimd const*, int)",
+                "SE::SeSchwarzPreconditioner::PreparePreconditioner(", "CPU_THREAD_NUM"):
+        assert sym in out, sym
+
+
+def test_facade_header_layouts_compile():
+    src = os.path.join(REPO, "tests", "cpp", "layout_check.cpp")
+    subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", INC, src], check=True)
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    import mas_amd
+    with pytest.raises(mas_amd.MasError, match="NO_DEVICE"):
+        mas_amd.SeSchwarzPreconditioner()
+
+
+def test_null_handle_and_bad_args():
+    import mas_amd
+    L = mas_amd.lib()
+    assert L.mas_destroy(None) == -1
+    assert L.mas_apply(None, None, None) == -1
+    assert L.mas_create(None, None) == -1
