@@ -128,6 +128,33 @@ int mas_apply_device(mas_handle h, float* d_z4, const float* d_r4, void* stream)
  * (up to 4096 applies) and reset the averages in mas_stats. */
 int mas_set_profiling(mas_handle h, int enable);
 
+/* ---- Morton-range sharding across `world` ranks (one process per GPU) ----
+ * Rank g owns a contiguous range of level-0 blocks (equal split).  Clusters
+ * never leave a level-0 bank, so its level-1 nodes form a contiguous segment
+ * [l1_begin, l1_end).  Per apply:
+ *   1. mas_apply_shard_restrict: R1 of the own segment -> d_seg[seg_max] float4
+ *   2. the caller allgathers every rank's d_seg into d_gathered[world][seg_max]
+ *      (RCCL over xGMI; torch.distributed all_gather_into_tensor)
+ *   3. mas_apply_shard_finish: coarse levels (own level-1 blocks, all blocks of
+ *      levels >= 2) and the own level-0 blocks; writes z for own vertices only.
+ * The union of the ranks' z entries is bitwise equal to mas_apply_device. */
+typedef struct {
+    int rank, world;
+    int fine_block_begin, fine_block_end; /* own level-0 blocks */
+    int vert_begin, vert_end;             /* own Morton-sorted vertices */
+    int l1_begin, l1_end;                 /* own level-1 nodes (level-1 local ids) */
+    int seg_max;                          /* padded segment length (max over ranks) */
+} mas_shard;
+
+/* Host-only planner (no device needed): nbanks = ceil(nV/32); l1_first[b] =
+ * first level-1 local id of level-0 bank b (b < nbanks), l1_first[nbanks] = n1. */
+int mas_shard_plan(int nV, const int* l1_first, int rank, int world, mas_shard* out);
+/* The same plan for a prepared handle. */
+int mas_shard_setup(mas_handle h, int rank, int world, mas_shard* out);
+int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r4, float* d_seg4, void* stream);
+int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gathered4, const float* d_r4,
+                           float* d_z4, void* stream);
+
 /* introspection / parity */
 int mas_get_info(mas_handle h, mas_info* out);
 int mas_get_stats(mas_handle h, mas_stats* out);

@@ -25,93 +25,11 @@
 // lane n+s) and one cross-half add.  No LDS, no atomics, no barriers.
 #include <vector>
 
-#include "layout.h"
-#include "mas_internal.h"
+#include "block_solve.h"
 
 namespace mas {
 
-constexpr int kApplyThreads = 256;  // 4 waves = 4 blocks per workgroup
-
-// One rotation step: out += G r_src, and lane dst receives G^T r_own.
-__device__ __forceinline__ void pair_step(float3& out, const float (&G)[9], float3 r, int src, int dst) {
-    const float mx = __shfl(r.x, src), my = __shfl(r.y, src), mz = __shfl(r.z, src);
-    out.x = __fmaf_rn(G[2], mz, __fmaf_rn(G[1], my, __fmaf_rn(G[0], mx, out.x)));
-    out.y = __fmaf_rn(G[5], mz, __fmaf_rn(G[4], my, __fmaf_rn(G[3], mx, out.y)));
-    out.z = __fmaf_rn(G[8], mz, __fmaf_rn(G[7], my, __fmaf_rn(G[6], mx, out.z)));
-    const float cx = __fmaf_rn(G[6], r.z, __fmaf_rn(G[3], r.y, __fmul_rn(G[0], r.x)));
-    const float cy = __fmaf_rn(G[7], r.z, __fmaf_rn(G[4], r.y, __fmul_rn(G[1], r.x)));
-    const float cz = __fmaf_rn(G[8], r.z, __fmaf_rn(G[5], r.y, __fmul_rn(G[2], r.x)));
-    out.x = __fadd_rn(out.x, __shfl(cx, dst));
-    out.y = __fadd_rn(out.y, __shfl(cy, dst));
-    out.z = __fadd_rn(out.z, __shfl(cz, dst));
-}
-
-// out = Inv_b r for the node this lane owns (layout.h).  g: the lane's
-// 72-float record, tl: its tail row (half 0, lanes 0..15; zero elsewhere).
-// Both halves return the same, complete result.
-__device__ __forceinline__ float3 block_solve(const float (&g)[kRecord], const float (&tl)[3], float3 r, int lane) {
-    const int n = lane & 31, hb = lane & 32;
-    const bool h1 = hb != 0;
-    float3 out;
-    {  // D(n) r, half 0 only
-        const float ox = __fmaf_rn(g[68], r.z, __fmaf_rn(g[67], r.y, __fmul_rn(g[66], r.x)));
-        const float oy = __fmaf_rn(g[70], r.z, __fmaf_rn(g[69], r.y, __fmul_rn(g[67], r.x)));
-        const float oz = __fmaf_rn(g[71], r.z, __fmaf_rn(g[70], r.y, __fmul_rn(g[68], r.x)));
-        out = h1 ? make_float3(0.f, 0.f, 0.f) : make_float3(ox, oy, oz);
-    }
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-        const int s = h1 ? 8 + k : 1 + k;
-        float G[9];
-#pragma unroll
-        for (int e = 0; e < 9; ++e) G[e] = g[9 * k + e];
-        pair_step(out, G, r, hb | ((n + s) & 31), hb | ((n - s) & 31));
-    }
-    {  // k = 7: half 1 regular s = 15; half 0 the s = 16 pair (p, p+16) as a
-       // rotation step with a per-lane 3x3: lane p = [row0; 0; row2],
-       // lane p+16 = row1 in column 1 (so it adds r_p.y row1 and returns row1.r).
-        const bool lo = n < 16;
-        const float w0 = g[63], w1 = g[64], w2 = g[65];
-        float G[9];
-        if (h1) {
-#pragma unroll
-            for (int e = 0; e < 9; ++e) G[e] = g[63 + e];
-        } else {
-            G[0] = lo ? w0 : 0.f;  G[1] = lo ? w1 : w0;   G[2] = lo ? w2 : 0.f;
-            G[3] = 0.f;            G[4] = lo ? 0.f : w1;  G[5] = 0.f;
-            G[6] = lo ? tl[0] : 0.f; G[7] = lo ? tl[1] : w2; G[8] = lo ? tl[2] : 0.f;
-        }
-        const int s = h1 ? 15 : 16;
-        pair_step(out, G, r, hb | ((n + s) & 31), hb | ((n - s) & 31));
-    }
-    // combine the halves (commutative add: both halves hold the same sum)
-    const int other = lane ^ 32;
-    out.x = __fadd_rn(out.x, __shfl(out.x, other));
-    out.y = __fadd_rn(out.y, __shfl(out.y, other));
-    out.z = __fadd_rn(out.z, __shfl(out.z, other));
-    return out;
-}
-
-template <bool NT = false>
-__device__ __forceinline__ void load_record(const float4* __restrict__ inv, int blk, int lane, float (&g)[kRecord],
-                                            float (&tl)[3]) {
-    const float4* b = inv + (size_t)blk * kBlockF4 + lane;
-#pragma unroll
-    for (int q = 0; q < kRecord / 4; ++q) {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        const v4f* bp = reinterpret_cast<const v4f*>(b + q * 64);
-        const v4f x = NT ? __builtin_nontemporal_load(bp) : *bp;
-        g[4 * q + 0] = x.x;
-        g[4 * q + 1] = x.y;
-        g[4 * q + 2] = x.z;
-        g[4 * q + 3] = x.w;
-    }
-    const float* t = reinterpret_cast<const float*>(inv + (size_t)blk * kBlockF4) + kMainFloats + 3 * (lane & 15);
-    tl[0] = t[0];
-    tl[1] = t[1];
-    tl[2] = t[2];
-    if (lane >= 16) tl[0] = tl[1] = tl[2] = 0.f;
-}
+static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThreads / 64); }
 
 // Fine blocks: gather r through the Morton map, solve, prolongate, scatter z.
 // The packed inverses are read exactly once per apply (630 MB at 1M, more
@@ -119,11 +37,11 @@ __device__ __forceinline__ void load_record(const float4* __restrict__ inv, int 
 // 98.8 vs 109.7 us per launch at 1M against default-policy loads (VAR = 0,
 // env MAS_FINE_VARIANT=0 keeps that variant for A/B runs).
 template <int NPROL, int VAR>
-__device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, int nFineBlk, int nV,
+__device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, int blk0, int nFineBlk, int nV,
                                                 const float4* __restrict__ r, const int4* __restrict__ vmap,
                                                 const float4* __restrict__ zc, int begin1, float4* __restrict__ z) {
     const int lane = threadIdx.x & 63, n = lane & 31;
-    const int blk = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
+    const int blk = blk0 + blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
     const bool bvalid = blk < nFineBlk;
     const int v = blk * 32 + n;
     const bool vvalid = bvalid && v < nV;
@@ -151,12 +69,12 @@ __device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, 
 
 
 template <int NPROL, int VAR>
-__global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __restrict__ inv, int nFineBlk, int nV,
-                                                             const float4* __restrict__ r,
+__global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __restrict__ inv, int blk0, int nFineBlk,
+                                                             int nV, const float4* __restrict__ r,
                                                              const int4* __restrict__ vmap,
                                                              const float4* __restrict__ zc, int begin1,
                                                              float4* __restrict__ z) {
-    solve_fine_body<NPROL, VAR>(inv, nFineBlk, nV, r, vmap, zc, begin1, z);
+    solve_fine_body<NPROL, VAR>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z);
 }
 
 // One coarse level l >= 1, one wave per 32-node block; lane n (half 0) owns
@@ -241,35 +159,38 @@ __global__ __launch_bounds__(256) void k_members(int nChild, int childBegin, con
     members[gn[childBegin + c] - begin1] = make_int2(c >> 5, (int)m);
 }
 
-static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThreads / 64); }
 
 template <int NPROL>
-static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int nFine, int nV, const float4* r,
-                          const int4* vmap, const float4* zc, int begin1, float4* z) {
-    if (var == 0) k_solve_fine<NPROL, 0><<<g, kApplyThreads, 0, s>>>(inv, nFine, nV, r, vmap, zc, begin1, z);
-    else k_solve_fine<NPROL, 1><<<g, kApplyThreads, 0, s>>>(inv, nFine, nV, r, vmap, zc, begin1, z);
+static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int blk0, int blkEnd, int nV,
+                          const float4* r, const int4* vmap, const float4* zc, int begin1, float4* z) {
+    if (var == 0) k_solve_fine<NPROL, 0><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
+    else k_solve_fine<NPROL, 1><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
 }
 
-static void launch_fine(int nprol, int var, int g, hipStream_t s, const float4* inv, int nFine, int nV,
-                        const float4* r, const int4* vmap, const float4* zc, int begin1, float4* z) {
-    switch (nprol) {
-        case 0: launch_fine_n<0>(var, g, s, inv, nFine, nV, r, vmap, zc, begin1, z); break;
-        case 1: launch_fine_n<1>(var, g, s, inv, nFine, nV, r, vmap, zc, begin1, z); break;
-        case 2: launch_fine_n<2>(var, g, s, inv, nFine, nV, r, vmap, zc, begin1, z); break;
-        default: launch_fine_n<3>(var, g, s, inv, nFine, nV, r, vmap, zc, begin1, z); break;
+// level-0 blocks [blk0, blkEnd) with prolongation of min(L,4)-1 coarse levels
+void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s) {
+    const int L = h->L;
+    const int g = cdiv(blkEnd - blk0, kApplyThreads / 64);
+    if (g <= 0) return;
+    const float4* inv = P<float4>(h->inv);
+    const int4* vmap = P<int4>(h->vmap);
+    const float4* zc = P<float4>(h->Zc);
+    const int begin1 = h->levelSize[3], nV = h->nV, var = h->fineVariant;
+    switch (L < 4 ? L - 1 : 3) {
+        case 0: launch_fine_n<0>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z); break;
+        case 1: launch_fine_n<1>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z); break;
+        case 2: launch_fine_n<2>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z); break;
+        default: launch_fine_n<3>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z); break;
     }
 }
 
-int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
-    const int L = h->L, nV = h->nV;
-    const int begin1 = h->levelSize[3];
+// coarse levels lFirst..L-1 with k_coarse (level 1 from the vertices)
+void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s) {
     const float4* inv = P<float4>(h->inv);
     float4* rc = P<float4>(h->Rc);
     float4* zc = P<float4>(h->Zc);
-    hipEvent_t* ev = nullptr;
-    if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
-    if (ev) hipEventRecord(ev[0], s);
-    for (int l = 1; l < L; ++l) {
+    const int begin1 = h->levelSize[3];
+    for (int l = lFirst; l < h->L; ++l) {
         const int cnt = h->levelSize[2 * l], beg = h->levelSize[2 * l + 1];
         const int nb = ceil32(cnt) / 32;
         if (l == 1)
@@ -279,13 +200,17 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
             k_coarse<false><<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int2>(h->members),
                                                                            h->levelSize[2 * (l - 1) + 1], nullptr,
                                                                            nullptr, rc, zc, begin1);
-        if (ev && l == 1) hipEventRecord(ev[1], s);
     }
-    if (ev && L == 1) hipEventRecord(ev[1], s);
+}
+
+int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
+    hipEvent_t* ev = nullptr;
+    if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
+    if (ev) hipEventRecord(ev[0], s);
+    if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
+    if (ev) hipEventRecord(ev[1], s);
     if (ev) hipEventRecord(ev[2], s);
-    const int4* vmap = P<int4>(h->vmap);
-    const int g = grid_for_blocks(h->nFineBlk);
-    launch_fine(L < 4 ? L - 1 : 3, h->fineVariant, g, s, inv, h->nFineBlk, nV, d_r, vmap, zc, begin1, d_z);
+    launch_fine(h, 0, h->nFineBlk, d_r, d_z, s);
     if (ev) hipEventRecord(ev[3], s);
     h->stats.apply_calls++;
     return hip_check(h, hipGetLastError(), "apply kernels");

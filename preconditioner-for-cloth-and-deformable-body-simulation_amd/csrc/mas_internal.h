@@ -73,7 +73,9 @@ struct mas_context {
     mas::Buffer dense, inv, slotTable;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab;
-    mas::Buffer Rc, Zc, members, coarseMask;
+    mas::Buffer Rc, Zc, members, coarseMask, shardOff;
+    std::vector<int> l1First;  // first level-1 local id per level-0 bank (+ n1), for sharding
+    int shardWorld = 0;
     // staging for host-pointer entry points
     mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
     // hipcub scratch
@@ -92,7 +94,7 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &Rc, &Zc, &members, &coarseMask, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &Rc, &Zc, &members, &coarseMask, &shardOff, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -124,6 +126,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
 int run_factor(mas_context* h, hipStream_t s);
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s);
 int upload_slot_table(mas_context* h);
+int prepare_apply_tables(mas_context* h, hipStream_t s);
+int compute_l1_first(mas_context* h, hipStream_t s);
 int copy_block_inverse(mas_context* h, int blk, float* out96);
 
 }  // namespace mas

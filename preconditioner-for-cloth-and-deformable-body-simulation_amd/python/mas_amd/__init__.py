@@ -31,7 +31,8 @@ STATUS = {0: "MAS_OK", -1: "MAS_ERR_ARG", -2: "MAS_ERR_HIP", -3: "MAS_ERR_CAPACI
 # every entry point declared in include/mas_capi.h
 EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_allocate", "mas_prepare",
            "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_get_info",
-           "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse"]
+           "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
+           "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish"]
 
 
 class mas_config(ctypes.Structure):
@@ -52,6 +53,14 @@ class mas_stats(ctypes.Structure):
                                                "prepare_assemble_ms", "prepare_factor_ms")] + \
                [("apply_calls", ctypes.c_int64), ("profiled_applies", ctypes.c_int64)] + \
                [(n, ctypes.c_double) for n in ("apply_ms_avg", "restrict_ms_avg", "coarse_ms_avg", "fine_ms_avg")]
+
+
+class mas_shard(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("rank", "world", "fine_block_begin", "fine_block_end", "vert_begin",
+                                            "vert_end", "l1_begin", "l1_end", "seg_max")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class MasError(RuntimeError):
@@ -93,6 +102,10 @@ def lib():
         L.mas_get_neighbors.argtypes = [P, P, P]
         L.mas_get_block_matrix.argtypes = [P, I, P]
         L.mas_get_block_inverse.argtypes = [P, I, P]
+        L.mas_shard_plan.argtypes = [I, P, I, I, ctypes.POINTER(mas_shard)]
+        L.mas_shard_setup.argtypes = [P, I, I, ctypes.POINTER(mas_shard)]
+        L.mas_apply_shard_restrict.argtypes = [P, I, I, P, P, P]
+        L.mas_apply_shard_finish.argtypes = [P, I, I, P, P, P, P]
         _lib = L
     return _lib
 
@@ -180,6 +193,20 @@ class SeSchwarzPreconditioner:
         """z, residual: torch cuda float32 tensors [nV, 4] (or raw device pointers)."""
         self._check(self._L.mas_apply_device(self.h, _ptr(z), _ptr(residual), _ptr(stream)), "PreconditioningDevice")
 
+    # ---- Morton-range sharding (include/mas_capi.h) ----
+    def shard_setup(self, rank, world) -> dict:
+        sh = mas_shard()
+        self._check(self._L.mas_shard_setup(self.h, rank, world, ctypes.byref(sh)), "shard_setup")
+        return sh.as_dict()
+
+    def shard_restrict(self, rank, world, r, seg, stream=None):
+        self._check(self._L.mas_apply_shard_restrict(self.h, rank, world, _ptr(r), _ptr(seg), _ptr(stream)),
+                    "shard_restrict")
+
+    def shard_finish(self, rank, world, gathered, r, z, stream=None):
+        self._check(self._L.mas_apply_shard_finish(self.h, rank, world, _ptr(gathered), _ptr(r), _ptr(z),
+                                                   _ptr(stream)), "shard_finish")
+
     # ---- introspection ----
     def set_profiling(self, on: bool):
         self._check(self._L.mas_set_profiling(self.h, int(on)), "set_profiling")
@@ -238,3 +265,13 @@ def from_mesh(mesh, max_levels=0, contacts=None, **kw) -> SeSchwarzPreconditione
         vf, vfC = contacts
         P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, vf, None, None, vfC)
     return P
+
+
+def shard_plan(nV, l1_first, rank, world) -> dict:
+    """Host-only Morton-range shard plan (mas_shard_plan; no device needed)."""
+    l1 = np.ascontiguousarray(l1_first, dtype=np.int32)
+    sh = mas_shard()
+    rc = lib().mas_shard_plan(nV, _ptr(l1), rank, world, ctypes.byref(sh))
+    if rc != MAS_OK:
+        raise MasError(f"mas_shard_plan failed: {STATUS.get(rc, rc)}")
+    return sh.as_dict()

@@ -1,0 +1,68 @@
+"""Sharded apply on one GPU with virtual ranks: every rank's restrict, an
+in-process 'allgather' (concatenation), every rank's finish into one z.  The
+union must be bitwise equal to the unsharded apply (same kernels, same
+arithmetic)."""
+import numpy as np
+import pytest
+
+from conftest import cloth, tet
+
+pytestmark = pytest.mark.gpu
+
+
+def _virtual_sharded(P, r, world):
+    import torch
+    plans = [P.shard_setup(g, world) for g in range(world)]
+    seg = plans[0]["seg_max"]
+    assert all(p["seg_max"] == seg for p in plans)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):  # torch ops and the library kernels on one stream
+        segs = [torch.zeros((seg, 4), dtype=torch.float32, device="cuda") for _ in range(world)]
+        for g in range(world):
+            P.shard_restrict(g, world, r, segs[g], s.cuda_stream)
+        gathered = torch.cat(segs, 0).contiguous()
+        z = torch.full_like(r, float("nan"))
+        for g in range(world):
+            P.shard_finish(g, world, gathered, r, z, s.cuda_stream)
+    s.synchronize()
+    # ranges tile the vertices exactly
+    assert plans[0]["vert_begin"] == 0 and plans[-1]["vert_end"] == r.shape[0]
+    for a, b in zip(plans, plans[1:]):
+        assert a["vert_end"] == b["vert_begin"] and a["l1_end"] == b["l1_begin"]
+    return z
+
+
+@pytest.mark.parametrize("kind,W,L,worlds", [("cloth", 64, 0, (1, 2, 3, 8)), ("cloth", 100, 1, (2, 5)),
+                                             ("tet", 16, 3, (2, 4)), ("cloth", 1024, 4, (2, 8))])
+def test_virtual_shards_bitwise(kind, W, L, worlds):
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(W) if kind == "cloth" else tet(W)
+    P = mas_amd.from_mesh(mesh, max_levels=L)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 3)).cuda()
+    z_ref = torch.zeros_like(r)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    P.PreconditioningDevice(z_ref, r, s.cuda_stream)
+    s.synchronize()
+    for world in worlds:
+        z = _virtual_sharded(P, r, world)
+        assert torch.equal(z, z_ref), (world, float((z - z_ref).abs().max()))
+
+
+def test_sharded_apply_helper_world1():
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    from mas_amd.distributed import ShardedApply
+    mesh = cloth(64)
+    P = mas_amd.from_mesh(mesh, max_levels=0)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 4)).cuda()
+    z = torch.zeros_like(r)
+    torch.cuda.synchronize()
+    S = ShardedApply(P, 0, 1)
+    s = torch.cuda.Stream()
+    S(z, r, s)
+    s.synchronize()
+    assert np.array_equal(z.cpu().numpy(), P.Preconditioning(None, r.cpu().numpy()))
