@@ -243,9 +243,9 @@ def main():
             "avg_launch_ms": round(st["fine_ms_avg"], 5),
         },
         "apply_breakdown_ms": {
-            "restrict": round(st["restrict_ms_avg"], 5),
-            "coarse_solve": round(st["coarse_ms_avg"], 5),
+            "pre_fine": round(st["pre_fine_ms_avg"], 5),
             "fine_solve": round(st["fine_ms_avg"], 5),
+            "post_fine": round(st["post_fine_ms_avg"], 5),
             "events_total": round(st["apply_ms_avg"], 5),
             "ms_per_step_with_kernel_events": round(elapsed_ev / args.steps * 1e3, 5),
         },

@@ -85,10 +85,10 @@ typedef struct {
     /* averages over the applies recorded while profiling was on (mas_set_profiling),
        measured with HIP events on the apply stream around each kernel group */
     int64_t profiled_applies;
-    double apply_ms_avg;       /* first restrict kernel start -> fine kernel end */
-    double restrict_ms_avg;    /* level 0->1 ... L-2->L-1 restriction kernels */
-    double coarse_ms_avg;      /* coarse-level block solves */
-    double fine_ms_avg;        /* fused gather + level-0 block solve + prolongation (dominant kernel) */
+    double apply_ms_avg;       /* apply start -> apply end on the caller stream */
+    double pre_fine_ms_avg;    /* before the fine kernel: coarse chain (serial mode) or fork (overlap mode) */
+    double fine_ms_avg;        /* the fine-level kernel: gather + level-0 block solves (+ prolongation) -- dominant */
+    double post_fine_ms_avg;   /* after it: join with the coarse chain + prolongation pass (overlap mode) */
 } mas_stats;
 
 /* lifecycle */

@@ -203,15 +203,74 @@ void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStre
     }
 }
 
+// z[s2o[v]] += Z1[a1]; += Z2[a2]; += Z3[a3] for v in [v0, v1) -- the
+// reference's CollectFinalZ order (.cpp:1706-1717) applied to z = Z0.
+template <int NPROL>
+__global__ __launch_bounds__(256) void k_prolong(int v0, int v1, const int4* __restrict__ vmap,
+                                                 const float4* __restrict__ zc, int begin1, float4* __restrict__ z) {
+    const int v = v0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= v1) return;
+    const int4 m = vmap[v];
+    float4 o = z[m.x];
+    if (NPROL >= 1) {
+        const float4 a = zc[m.y - begin1];
+        o.x = __fadd_rn(o.x, a.x); o.y = __fadd_rn(o.y, a.y); o.z = __fadd_rn(o.z, a.z);
+    }
+    if (NPROL >= 2) {
+        const float4 a = zc[m.z - begin1];
+        o.x = __fadd_rn(o.x, a.x); o.y = __fadd_rn(o.y, a.y); o.z = __fadd_rn(o.z, a.z);
+    }
+    if (NPROL >= 3) {
+        const float4 a = zc[m.w - begin1];
+        o.x = __fadd_rn(o.x, a.x); o.y = __fadd_rn(o.y, a.y); o.z = __fadd_rn(o.z, a.z);
+    }
+    z[m.x] = o;
+}
+
+void launch_prolong(mas_context* h, int v0, int v1, float4* z, hipStream_t s) {
+    const int nprol = h->L < 4 ? h->L - 1 : 3;
+    const int g = cdiv(v1 - v0, 256);
+    if (g <= 0 || nprol == 0) return;
+    const int4* vmap = P<int4>(h->vmap);
+    const float4* zc = P<float4>(h->Zc);
+    const int b1 = h->levelSize[3];
+    if (nprol == 1) k_prolong<1><<<g, 256, 0, s>>>(v0, v1, vmap, zc, b1, z);
+    else if (nprol == 2) k_prolong<2><<<g, 256, 0, s>>>(v0, v1, vmap, zc, b1, z);
+    else k_prolong<3><<<g, 256, 0, s>>>(v0, v1, vmap, zc, b1, z);
+}
+
+// Fine blocks without prolongation (z = Z0) for [blk0, blkEnd).
+void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s) {
+    const int g = cdiv(blkEnd - blk0, kApplyThreads / 64);
+    if (g <= 0) return;
+    launch_fine_n<0>(h->fineVariant, g, s, P<float4>(h->inv), blk0, blkEnd, h->nV, r, P<int4>(h->vmap),
+                     P<float4>(h->Zc), h->levelSize[3], z);
+}
+
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     hipEvent_t* ev = nullptr;
     if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
     if (ev) hipEventRecord(ev[0], s);
-    if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
-    if (ev) hipEventRecord(ev[1], s);
-    if (ev) hipEventRecord(ev[2], s);
-    launch_fine(h, 0, h->nFineBlk, d_r, d_z, s);
-    if (ev) hipEventRecord(ev[3], s);
+    if (h->L > 1 && h->overlap) {
+        // coarse chain on the side stream, concurrent with the fine blocks;
+        // join, then the prolongation pass (bitwise equal to the fused form)
+        hipEventRecord(h->evFork, s);
+        hipStreamWaitEvent(h->stream2, h->evFork, 0);
+        launch_coarse_levels(h, 1, d_r, h->stream2);
+        hipEventRecord(h->evJoin, h->stream2);
+        if (ev) hipEventRecord(ev[1], s);
+        launch_fine_z0(h, 0, h->nFineBlk, d_r, d_z, s);
+        if (ev) hipEventRecord(ev[2], s);
+        hipStreamWaitEvent(s, h->evJoin, 0);
+        launch_prolong(h, 0, h->nV, d_z, s);
+        if (ev) hipEventRecord(ev[3], s);
+    } else {
+        if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
+        if (ev) hipEventRecord(ev[1], s);
+        launch_fine(h, 0, h->nFineBlk, d_r, d_z, s);
+        if (ev) hipEventRecord(ev[2], s);
+        if (ev) hipEventRecord(ev[3], s);
+    }
     h->stats.apply_calls++;
     return hip_check(h, hipGetLastError(), "apply kernels");
 }

@@ -182,8 +182,8 @@ int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gat
         launch_coarse_levels(h, 2, r, s);
     }
     if (ev) hipEventRecord(ev[1], s);
-    if (ev) hipEventRecord(ev[2], s);
     launch_fine(h, sh.fine_block_begin, sh.fine_block_end, r, z, s);
+    if (ev) hipEventRecord(ev[2], s);
     if (ev) hipEventRecord(ev[3], s);
     h->stats.apply_calls++;
     return hip_check(h, hipGetLastError(), "shard finish");

@@ -90,6 +90,13 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     }
     for (auto& e : h->ev) hipEventCreate(&e);
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
+    if (const char* v = std::getenv("MAS_OVERLAP")) h->overlap = std::atoi(v);
+    if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess) {
+        mas_destroy(h);
+        return MAS_ERR_HIP;
+    }
     int rc = upload_slot_table(h);
     if (rc != MAS_OK) {
         mas_destroy(h);
@@ -107,6 +114,12 @@ int mas_destroy(mas_handle h) {
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
     for (auto& e : h->prof) hipEventDestroy(e);
+    if (h->evFork) hipEventDestroy(h->evFork);
+    if (h->evJoin) hipEventDestroy(h->evJoin);
+    if (h->stream2) {
+        hipStreamSynchronize(h->stream2);
+        hipStreamDestroy(h->stream2);
+    }
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return MAS_OK;
@@ -200,7 +213,7 @@ int mas_set_profiling(mas_handle h, int enable) {
     h->profiling = enable != 0;
     h->profRecorded = 0;
     h->stats.profiled_applies = 0;
-    h->stats.apply_ms_avg = h->stats.restrict_ms_avg = h->stats.coarse_ms_avg = h->stats.fine_ms_avg = 0.0;
+    h->stats.apply_ms_avg = h->stats.pre_fine_ms_avg = h->stats.fine_ms_avg = h->stats.post_fine_ms_avg = 0.0;
     return MAS_OK;
 }
 
@@ -235,15 +248,15 @@ int mas_get_stats(mas_handle h, mas_stats* out) {
             float a = 0, r = 0, c = 0, f = 0;
             hipEventElapsedTime(&a, e[0], e[3]);
             hipEventElapsedTime(&r, e[0], e[1]);
-            hipEventElapsedTime(&c, e[1], e[2]);
-            hipEventElapsedTime(&f, e[2], e[3]);
+            hipEventElapsedTime(&f, e[1], e[2]);
+            hipEventElapsedTime(&c, e[2], e[3]);
             sa += a; sr += r; sc += c; sf += f;
         }
         h->stats.profiled_applies = n;
         h->stats.apply_ms_avg = sa / n;
-        h->stats.restrict_ms_avg = sr / n;
-        h->stats.coarse_ms_avg = sc / n;
+        h->stats.pre_fine_ms_avg = sr / n;
         h->stats.fine_ms_avg = sf / n;
+        h->stats.post_fine_ms_avg = sc / n;
     }
     *out = h->stats;
     return MAS_OK;
