@@ -22,10 +22,11 @@
 //   k_fold_entries  one thread per coarse entry (row, col), records sorted
 //                 stably by (row, col): entry += mat in (u, k) order
 //   k_diag1       one thread per level-0 bank: diag(anc1(u)) += od(u) (.cpp:1309-1312)
-//   k_table       one thread per level-l node (l >= 2): the diagTable fold
-//                 (.cpp:1299-1343): over member vertices in order, level-(l-1)
+//   k_term_*, k_table_fold  the diagTable fold (.cpp:1299-1343) per level-l
+//                 node (l >= 2): over member vertices in order, level-(l-1)
 //                 edge mats and (l = 2) od(u); then the children's tables in
-//                 id order; diag += table.
+//                 id order; diag += table.  Terms are flattened in parallel,
+//                 then folded strictly left by one wave per node.
 // Contact stencils (only present in the contact configuration) still
 // accumulate with fp32 atomics, as the reference does at CPU_THREAD_NUM > 1.
 #include <hipcub/hipcub.hpp>
@@ -242,51 +243,93 @@ __global__ __launch_bounds__(256) void k_bounds(int n, const int* __restrict__ s
 }
 
 // diagTable fold for level l >= 2, one thread per level-l node P.
-__global__ __launch_bounds__(256) void k_table(int l, int L, int count, int begin, int beginPrev,
-                                               const int* __restrict__ vlist, const int* __restrict__ voff,
-                                               const int* __restrict__ cstPrev2, const int* __restrict__ gn,
-                                               const int* __restrict__ recOff, const EdgeRec* __restrict__ rec,
-                                               const float* __restrict__ off9, const float* __restrict__ od,
-                                               float* __restrict__ tab, float* __restrict__ dense) {
-    const int local = blockIdx.x * blockDim.x + threadIdx.x;
-    if (local >= count) return;
-    const int P = begin + local;
-    float t[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    bool present = false;
-    const int b = voff[local], e = voff[local + 1];
-    for (int i = b; i < e; ++i) {
-        const int u = vlist[i];
-        for (int j = recOff[u]; j < recOff[u + 1]; ++j) {
-            const EdgeRec r = rec[j];
-            if (r.lam != l - 1) continue;
-            const float* m = off9 + 9 * (size_t)r.mat;
-            for (int rr = 0; rr < 3; ++rr)
-                for (int c = 0; c < 3; ++c) t[rr * 3 + c] = __fadd_rn(t[rr * 3 + c], m[c * 3 + rr]);
-            present = true;
-        }
-        if (l == 2) {
-            const float* a = od + 9 * (size_t)u;
-            for (int q = 0; q < 9; ++q) t[q] = __fadd_rn(t[q], a[q]);
-            present = true;
-        }
+// diagTable fold (.cpp:1299-1343), parallelised over the terms but folded
+// strictly left in the reference's order.  For level l the ordered term list
+// of node P is: for each member vertex u in ascending order, u's edge records
+// with lam == l-1 (in (u, k) order) and, for l == 2, od(u); then (l >= 3) the
+// level-(l-1) tables of the children in id order.  k_term_count / scan /
+// k_term_write flatten the vertex part into one index array (>= 0: off9
+// matrix, < 0: od of vertex -t-1); k_table_fold folds it with one wave per
+// node: the wave stages 256 terms at a time in LDS (coalesced loads, 4 terms
+// in flight per lane) and lanes 0..8 each fold one of the nine entries.
+__global__ __launch_bounds__(256) void k_term_count(int l, int nV, const int* __restrict__ vlist,
+                                                    const int* __restrict__ recOff, const EdgeRec* __restrict__ rec,
+                                                    int* __restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > nV) return;
+    if (i == nV) { cnt[i] = 0; return; }
+    const int u = vlist[i];
+    int c = (l == 2) ? 1 : 0;
+    for (int j = recOff[u]; j < recOff[u + 1]; ++j) c += (rec[j].lam == l - 1);
+    cnt[i] = c;
+}
+
+__global__ __launch_bounds__(256) void k_term_write(int l, int nV, const int* __restrict__ vlist,
+                                                    const int* __restrict__ recOff, const EdgeRec* __restrict__ rec,
+                                                    const int* __restrict__ termOff, int* __restrict__ terms) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nV) return;
+    const int u = vlist[i];
+    int o = termOff[i];
+    for (int j = recOff[u]; j < recOff[u + 1]; ++j) {
+        const EdgeRec r = rec[j];
+        if (r.lam == l - 1) terms[o++] = r.mat;
     }
-    if (l >= 3) {  // pushes of the level-(l-1) tables, children in id order (.cpp:1333-1341)
-        const int u0 = vlist[b];
-        const int childLocal = cstPrev2[u0];  // level-(l-1) local id of the first member
+    if (l == 2) terms[o] = -(u + 1);
+}
+
+constexpr int kFoldChunk = 256;
+
+__global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, int beginPrev,
+                                                   const int* __restrict__ vlist, const int* __restrict__ voff,
+                                                   const int* __restrict__ termOff, const int* __restrict__ terms,
+                                                   const int* __restrict__ cstPrev2, const int* __restrict__ gn,
+                                                   const float* __restrict__ off9, const float* __restrict__ od,
+                                                   float* __restrict__ tab, float* __restrict__ dense) {
+    __shared__ float st[kFoldChunk * 9];
+    const int local = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int P = begin + local;
+    const int vb = voff[local], ve = voff[local + 1];
+    const int tb = termOff[vb], te = termOff[ve];
+    // lane q < 9 folds entry q = (row, col) = (q / 3, q % 3); off9 is column-major
+    const int q = lane < 9 ? lane : 0;
+    float acc = 0.f;
+    for (int base = tb; base < te; base += kFoldChunk) {
+        const int n = min(kFoldChunk, te - base);
+#pragma unroll
+        for (int m = 0; m < kFoldChunk / 64; ++m) {
+            const int k = m * 64 + lane;
+            if (k < n) {
+                const int t = terms[base + k];
+                const float* src = t >= 0 ? off9 + 9 * (size_t)t : od + 9 * (size_t)(-t - 1);
+                const bool colMajor = t >= 0;
+#pragma unroll
+                for (int e = 0; e < 9; ++e) st[k * 9 + e] = src[colMajor ? (e % 3) * 3 + e / 3 : e];
+            }
+        }
+        __syncthreads();
+        if (lane < 9)
+            for (int k = 0; k < n; ++k) acc = __fadd_rn(acc, st[k * 9 + q]);
+        __syncthreads();
+    }
+    bool present = te > tb;
+    if (l >= 3 && ve > vb) {  // pushes of the level-(l-1) tables, children in id order (.cpp:1333-1341)
+        const int childLocal = cstPrev2[vlist[vb]];  // level-(l-1) local id of the first member
         const int bankBase = beginPrev + (childLocal & ~31);
         for (int j = 0; j < 32; ++j) {
             const int c = bankBase + j;
             if (gn[c] != P) continue;
-            const float* a = tab + 9 * (size_t)c;
-            for (int q = 0; q < 9; ++q) t[q] = __fadd_rn(t[q], a[q]);
+            if (lane < 9) acc = __fadd_rn(acc, tab[9 * (size_t)c + q]);
             present = true;
         }
     }
-    for (int q = 0; q < 9; ++q) tab[9 * (size_t)P + q] = t[q];
-    if (present) {
-        float* d = entry(dense, (unsigned)P, (unsigned)P);
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) d[r * 96 + c] = __fadd_rn(d[r * 96 + c], t[r * 3 + c]);
+    if (lane < 9) {
+        tab[9 * (size_t)P + q] = acc;
+        if (present) {
+            float* d = entry(dense, (unsigned)P, (unsigned)P) + (q / 3) * 96 + q % 3;
+            *d = __fadd_rn(*d, acc);
+        }
     }
 }
 
@@ -356,7 +399,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
 
     // diagTable folds, levels 2..L-1
     if ((rc = ensure(h, h->vkeys, (size_t)nV * 4)) || (rc = ensure(h, h->vlist, (size_t)nV * 4)) ||
-        (rc = ensure(h, h->voff, (size_t)(nV + 1) * 4)))
+        (rc = ensure(h, h->voff, (size_t)(nV + 1) * 4)) || (rc = ensure(h, h->termCnt, (size_t)(nV + 1) * 4)) ||
+        (rc = ensure(h, h->termOff, (size_t)(nV + 1) * 4)) || (rc = ensure(h, h->terms, ((size_t)nRec + nV) * 4)))
         return rc;
     for (int l = 2; l < L; ++l) {
         const int count = h->levelSize[2 * l], begin = h->levelSize[2 * l + 1];
@@ -373,9 +417,21 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                             "vertex-list sort")))
             return rc;
         k_bounds<<<cdiv(nV, 256), 256, 0, s>>>(nV, P<int>(h->vkeys), count, P<int>(h->voff));
-        k_table<<<cdiv(count, 256), 256, 0, s>>>(l, L, count, begin, beginPrev, P<int>(h->vlist), P<int>(h->voff),
-                                                 cstPrev2, gn, P<int>(h->recOff), rec, d_off9, P<float>(h->od),
-                                                 P<float>(h->tab), dense);
+        k_term_count<<<cdiv(nV + 1, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff), rec,
+                                                       P<int>(h->termCnt));
+        tmp = 0;
+        hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, P<int>(h->termCnt), P<int>(h->termOff), nV + 1, s);
+        if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
+        if ((rc = hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, P<int>(h->termCnt),
+                                                                P<int>(h->termOff), nV + 1, s),
+                            "term scan")))
+            return rc;
+        k_term_write<<<cdiv(nV, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff), rec,
+                                                   P<int>(h->termOff), P<int>(h->terms));
+        if (count > 0)
+            k_table_fold<<<count, 64, 0, s>>>(l, count, begin, beginPrev, P<int>(h->vlist), P<int>(h->voff),
+                                              P<int>(h->termOff), P<int>(h->terms), cstPrev2, gn, d_off9,
+                                              P<float>(h->od), P<float>(h->tab), dense);
     }
     return hip_check(h, hipGetLastError(), "assembly kernels");
 }

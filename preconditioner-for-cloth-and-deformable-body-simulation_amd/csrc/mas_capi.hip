@@ -90,6 +90,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     }
     for (auto& e : h->ev) hipEventCreate(&e);
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
+    if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_OVERLAP")) h->overlap = std::atoi(v);
     if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||

@@ -60,6 +60,7 @@ struct mas_context {
     int overlap = 0;      // 1: coarse chain on stream2 beside the fine blocks (measured slower: 150.8 vs 124.3 us at 1M; env MAS_OVERLAP)
     hipStream_t stream2 = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;
+    int factorVariant = 1;  // 1 = register-resident rows (k_factor_reg); env MAS_FACTOR_VARIANT=0: LDS rows
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     int levelSize[2 * 9] = {};
@@ -75,7 +76,7 @@ struct mas_context {
     mas::Buffer cst, goingNext, vmap, coarseTables;
     mas::Buffer dense, inv, slotTable;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
-    mas::Buffer vkeys, vlist, voff, tab;
+    mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff;
     std::vector<int> l1First;  // first level-1 local id per level-0 bank (+ n1), for sharding
     int shardWorld = 0;
@@ -97,7 +98,7 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &Rc, &Zc, &members, &coarseMask, &shardOff, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
