@@ -122,7 +122,18 @@ def main():
     P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts, device=local)
     setup_s = time.perf_counter() - t0
     info = P.info()
-    st0 = P.stats()
+    st_first = P.stats()
+    # steady-state Prepare (the per-solve call in a simulator): buffers exist,
+    # repeat it and keep the median; the first call also allocates
+    reps = []
+    for _ in range(3):
+        if contacts is None:
+            P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
+        else:
+            P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, contacts[0], None, None,
+                                    contacts[1])
+        reps.append(P.stats())
+    st0 = sorted(reps, key=lambda d: d["prepare_ms"])[1]
     seed = 0x5EED + CONFIG_ORDER.index(args.config)
     r_np = meshgen.residual(mesh.nV, seed)
     r = torch.from_numpy(r_np).cuda()
@@ -252,6 +263,7 @@ def main():
         "apply_algorithmic_GBps": round(apply_bytes / (t_max / args.steps) / 1e9, 1),
         "apply_bytes": apply_bytes,
         "prepare_ms": round(st0["prepare_ms"], 3),
+        "prepare_first_call_ms": round(st_first["prepare_ms"], 3),
         "prepare_breakdown_ms": {"levels": round(st0["prepare_levels_ms"], 3),
                                  "assemble": round(st0["prepare_assemble_ms"], 3),
                                  "factor": round(st0["prepare_factor_ms"], 3)},

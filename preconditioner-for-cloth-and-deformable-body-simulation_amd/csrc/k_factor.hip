@@ -1,19 +1,23 @@
 // k_factor.hip -- batched no-pivot LDL^T of the 96x96 subdomain blocks and the
 // packed symmetric inverse (LDLtInverse512, .cpp:1347-1546).
 //
-// One workgroup (128 threads) per block; the block lives in LDS (96 x 100
-// floats: 16-byte aligned rows, conflict-free ds_read_b128 across rows).
-//   1. load + zero-diagonal -> identity (.cpp:1365-1368)
+// The reference arithmetic, per block:
+//   1. zero-diagonal node -> identity 3x3 (.cpp:1365-1368)
 //   2. row-oriented elimination x = 0..95, rows skip a zero multiplier, the
 //      row update runs over all 96 columns with FMA so the strict lower part
-//      accumulates L^-1 (.cpp:1395-1415) -- thread y owns row y and updates it
-//      with 24 float4 FMAs against the broadcast pivot row
+//      accumulates L^-1 (.cpp:1395-1415)
 //   3. D^-1 by IEEE division (.cpp:1429-1433)
 //   4. Inv[i][j] = sum_{k = 95 .. j} fma(D^-1_k, L^-1[k][i] * L^-1[k][j], acc),
-//      the reference's accumulation order (.cpp:1437-1495), written in the
-//      node-pair layout of layout.h (coalesced stores)
-// Operation for operation this is the reference arithmetic, so identical
-// input blocks give bit-identical inverses.
+//      the reference's accumulation order (.cpp:1437-1495), stored in the
+//      node-pair layout of layout.h
+// Two kernels perform exactly these operations on every element in this
+// order, so identical input blocks give bit-identical inverses:
+//   k_factor     one 128-thread workgroup per block, block in LDS, thread y
+//                owns row y (MAS_FACTOR_VARIANT=0; LDS-bandwidth bound:
+//                every FMA reads its pivot value from LDS) -- 15.0 ms at 1M
+//   k_factor_rb  (default) one wave per block, rows in VGPRs in 6x24 lane
+//                tiles, the pivot row broadcast through LDS, multipliers and
+//                quotients through DPP -- 2.3 ms at 1M (profiles/round1/ab)
 #include <vector>
 
 #include "layout.h"
@@ -23,6 +27,9 @@ namespace mas {
 
 constexpr int kLda = 100;
 constexpr int kFactorThreads = 128;
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+static_assert(kDenseFloats / 4 % kFactorThreads == 0, "factor load tiling");
 
 __global__ __launch_bounds__(kFactorThreads) void k_factor(const float* __restrict__ dense,
                                                           const unsigned* __restrict__ slotTable,
@@ -79,109 +86,145 @@ __global__ __launch_bounds__(kFactorThreads) void k_factor(const float* __restri
     }
 }
 
-// One elimination step with the step index x a compile-time constant, so the
-// row stays in VGPRs (v[x] is a static register; a runtime x would demote the
-// row to scratch).  Elim<0>::run expands all 96 steps.
-template <int X>
-__device__ __forceinline__ void elim_step(float (&v)[96], float (*piv)[96], float* dinv, bool has, int row) {
-    float* pr = piv[X & 1];
-    if (has && row == X) {  // the owner publishes its final row
-#pragma unroll
-        for (int c4 = 0; c4 < 24; ++c4)
-            *reinterpret_cast<float4*>(&pr[4 * c4]) = make_float4(v[4 * c4], v[4 * c4 + 1], v[4 * c4 + 2], v[4 * c4 + 3]);
-        dinv[X] = __fdiv_rn(1.0f, v[X]);
-    }
-    __syncthreads();
-    if (has && row > X) {
-        const float a = v[X];
-        if (a != 0.0f) {
-            const float r = __fdiv_rn(-a, pr[X]);
-#pragma unroll
-            for (int c4 = 0; c4 < 24; ++c4) {
-                const float4 p = *reinterpret_cast<const float4*>(&pr[4 * c4]);
-                v[4 * c4] = __fmaf_rn(r, p.x, v[4 * c4]);
-                v[4 * c4 + 1] = __fmaf_rn(r, p.y, v[4 * c4 + 1]);
-                v[4 * c4 + 2] = __fmaf_rn(r, p.z, v[4 * c4 + 2]);
-                v[4 * c4 + 3] = __fmaf_rn(r, p.w, v[4 * c4 + 3]);
-            }
-            v[X] = r;
-        }
+template <int SEL>
+__device__ __forceinline__ float quad_bcast_c(float x) {
+    constexpr int ctrl = SEL | (SEL << 2) | (SEL << 4) | (SEL << 6);  // quad_perm [SEL, SEL, SEL, SEL]
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), ctrl, 0xf, 0xf, false));
+}
+// sel is a constant after unrolling; the switch folds away
+__device__ __forceinline__ float quad_bcast(float x, int sel) {
+    switch (sel & 3) {
+        case 0: return quad_bcast_c<0>(x);
+        case 1: return quad_bcast_c<1>(x);
+        case 2: return quad_bcast_c<2>(x);
+        default: return quad_bcast_c<3>(x);
     }
 }
 
 template <int X>
-struct Elim {
-    static __device__ __forceinline__ void run(float (&v)[96], float (*piv)[96], float* dinv, bool has, int row) {
-        elim_step<X>(v, piv, dinv, has, row);
-        Elim<X + 1>::run(v, piv, dinv, has, row);
+__device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float* dinv, int rg, int cg) {
+    constexpr int mX = X / 16, rX = X % 16, cgX = X / 24, cX = X % 24;
+    constexpr int mLo = (X < 15) ? 0 : (X - 15) / 16 + 1;
+    float* pr = piv;  // one buffer: a single wave's LDS operations complete in order
+    if (rg == rX) {
+#pragma unroll
+        for (int c4 = 0; c4 < 6; ++c4)
+            *reinterpret_cast<float4*>(&pr[24 * cg + 4 * c4]) =
+                make_float4(v[mX][4 * c4], v[mX][4 * c4 + 1], v[mX][4 * c4 + 2], v[mX][4 * c4 + 3]);
+        if (cg == cgX) dinv[X] = __fdiv_rn(1.0f, v[mX][cX]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if constexpr (mLo <= 5) {
+        const float pd = pr[X];
+        float a[6], r[6];
+#pragma unroll
+        for (int m = mLo; m < 6; ++m) a[m] = quad_bcast(v[m][cX], cgX);
+        // lane cg divides for rows m = mLo + cg and mLo + 4 + cg
+        float q0 = 0.f, q1 = 0.f;
+        {
+            const int m0 = mLo + cg, m1 = mLo + 4 + cg;
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int m = mLo; m < 6; ++m) {
+                a0 = (m == m0) ? a[m] : a0;
+                a1 = (m == m1) ? a[m] : a1;
+            }
+            const bool act0 = m0 < 6 && rg + 16 * m0 > X && a0 != 0.0f;
+            const bool act1 = m1 < 6 && rg + 16 * m1 > X && a1 != 0.0f;
+            if (act0) q0 = __fdiv_rn(-a0, pd);
+            if (act1) q1 = __fdiv_rn(-a1, pd);
+        }
+#pragma unroll
+        for (int m = mLo; m < 6; ++m) r[m] = quad_bcast((m - mLo) < 4 ? q0 : q1, (m - mLo) & 3);
+        // the pivot row in two halves of 12 (register budget: 2 waves per SIMD)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            float p[12];
+#pragma unroll
+            for (int c4 = 0; c4 < 3; ++c4) {
+                const float4 q = *reinterpret_cast<const float4*>(&pr[24 * cg + 12 * hh + 4 * c4]);
+                p[4 * c4] = q.x;
+                p[4 * c4 + 1] = q.y;
+                p[4 * c4 + 2] = q.z;
+                p[4 * c4 + 3] = q.w;
+            }
+#pragma unroll
+            for (int m = mLo; m < 6; ++m)
+#pragma unroll
+                for (int c = 0; c < 12; ++c) v[m][12 * hh + c] = __fmaf_rn(r[m], p[c], v[m][12 * hh + c]);
+            if (hh == 0) {  // keep the second half's loads behind the first half's updates
+#pragma unroll
+                for (int m = mLo; m < 6; ++m)
+#pragma unroll
+                    for (int c = 0; c < 12; c += 2) {
+                        v2f q = {v[m][c], v[m][c + 1]};
+                        asm volatile("" : "+v"(q)::"memory");
+                        v[m][c] = q.x;
+                        v[m][c + 1] = q.y;
+                    }
+            }
+        }
+#pragma unroll
+        for (int m = mLo; m < 6; ++m) {
+            // A[row][X] = r where the reference ran the update (row > X, a != 0)
+            const bool upd = (cg == cgX) && (rg + 16 * m > X) && (a[m] != 0.0f);
+            v[m][cX] = upd ? r[m] : v[m][cX];
+        }
+    }
+    // Pin the step's results here: otherwise LLVM sinks the updates of rows
+    // not needed by the next pivot into later steps and every step's pivot
+    // row stays live (hundreds of VGPRs, then scratch).
+#pragma unroll
+    for (int m = mLo; m < 6; ++m)
+#pragma unroll
+        for (int c = 0; c < 24; c += 2) {  // as register pairs, so the updates stay v_pk_fma_f32
+            v2f q = {v[m][c], v[m][c + 1]};
+            asm volatile("" : "+v"(q));
+            v[m][c] = q.x;
+            v[m][c + 1] = q.y;
+        }
+}
+
+template <int X>
+struct ElimRB {
+    static __device__ __forceinline__ void run(float (&v)[6][24], float* piv, float* dinv, int rg, int cg) {
+        rb_step<X>(v, piv, dinv, rg, cg);
+        ElimRB<X + 1>::run(v, piv, dinv, rg, cg);
     }
 };
 template <>
-struct Elim<96> {
-    static __device__ __forceinline__ void run(float (&)[96], float (*)[96], float*, bool, int) {}
+struct ElimRB<96> {
+    static __device__ __forceinline__ void run(float (&)[6][24], float*, float*, int, int) {}
 };
 
-// Register-resident variant (default).  Same operations on every element in
-// the same order as k_factor above, rescheduled for CDNA4:
-//   * thread -> row: wave 0 lanes own rows 32..63+32 (busy for all 95 steps),
-//     wave 1 lanes 0..31 own rows 0..31 (busy only for steps < 32), so no
-//     lane of wave 0 idles on a row that is already final;
-//   * each row lives in 96 VGPRs for the whole elimination (the x loop is
-//     fully unrolled, so v[x] is a static register); step x's owner publishes
-//     its final row to a double-buffered LDS pivot row -> one barrier per step
-//     and no LDS traffic for the row updates;
-//   * D^-1 is computed by the pivot owner when it publishes;
-//   * the inverse is formed in 4x4 tiles (i-block <= j-block) from the
-//     eliminated matrix in LDS with unit diagonal: per k two ds_read_b128 and
-//     16 (fmul, fma) pairs, k descending from 95 as in the reference; results
-//     go to the free strict upper triangle of A (never read as L^-1) and
-//     invDiag, then out through the slot table with coalesced stores.
-__global__ __launch_bounds__(kFactorThreads) void k_factor_reg(const float* __restrict__ dense,
-                                                              const unsigned* __restrict__ slotTable,
-                                                              float* __restrict__ inv) {
-    __shared__ __attribute__((aligned(16))) float A[96 * kLda];
-    __shared__ __attribute__((aligned(16))) float piv[2][96];
-    __shared__ float dinv[96];
-    __shared__ float invDiag[96];
-    const int t = threadIdx.x;
-    const size_t blk = blockIdx.x;
-    const float4* src = reinterpret_cast<const float4*>(dense + blk * kDenseFloats);
-    for (int q = t; q < kDenseFloats / 4; q += kFactorThreads) {
-        const int row = q / 24, c4 = q % 24;
-        *reinterpret_cast<float4*>(&A[row * kLda + 4 * c4]) = src[q];
-    }
-    __syncthreads();
-    if (t < 32 && A[(3 * t) * kLda + 3 * t] == 0.0f) {  // .cpp:1365-1368
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) A[(3 * t + i) * kLda + 3 * t + j] = (i == j) ? 1.f : 0.f;
-    }
-    __syncthreads();
-    const bool has = t < 96;
-    const int row = t < 64 ? 32 + t : t - 64;
-    float v[96];
-    if (has) {
-#pragma unroll
-        for (int c4 = 0; c4 < 24; ++c4) {
-            const float4 q = *reinterpret_cast<const float4*>(&A[row * kLda + 4 * c4]);
-            v[4 * c4] = q.x;
-            v[4 * c4 + 1] = q.y;
-            v[4 * c4 + 2] = q.z;
-            v[4 * c4 + 3] = q.w;
-        }
-    }
-    Elim<0>::run(v, piv, dinv, has, row);
-    if (has) {
-#pragma unroll
-        for (int c4 = 0; c4 < 24; ++c4)
-            *reinterpret_cast<float4*>(&A[row * kLda + 4 * c4]) =
-                make_float4(v[4 * c4], v[4 * c4 + 1], v[4 * c4 + 2], v[4 * c4 + 3]);
-    }
-    __syncthreads();
-    if (has) A[t * kLda + t] = 1.0f;  // M[k][k] = 1 (the reference's k == i / k == j cases)
-    __syncthreads();
-    // 300 tiles (I <= J) of 4x4 entries; Inv[i][j] = sum_{k = 95 .. j} fma(dinv_k, M[k][i] * M[k][j], acc)
-    for (int tile = t; tile < 300; tile += kFactorThreads) {
-        int J = 0, rem = tile;  // tile -> (I, J), J-major: J has J + 1 tiles
+// Zero diagonal -> identity node block (.cpp:1365-1368), applied in place to
+// the assembled blocks before the register-resident factor kernels (which
+// never see the whole block in one place).  mas_get_block_matrix reports the
+// same rule, so the stored blocks read back unchanged.
+__global__ __launch_bounds__(256) void k_identity_fix(float* __restrict__ dense, int nNodes) {
+    const int node = blockIdx.x * blockDim.x + threadIdx.x;
+    if (node >= nNodes) return;
+    float* d = dense + (size_t)(node >> 5) * kDenseFloats + (3 * (node & 31)) * 96 + 3 * (node & 31);
+    if (*d != 0.0f) return;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) d[i * 96 + j] = (i == j) ? 1.f : 0.f;
+}
+
+// Packed lower-triangular M in LDS: row k holds columns [0, ceil4(k+1)), so the
+// formation's float4 reads stay aligned; 4 800 floats = 19.2 KB.
+__device__ __forceinline__ int m_row(int k) {
+    const int g = k >> 2;
+    return 8 * g * (g + 1) + (k & 3) * 4 * (g + 1);
+}
+constexpr int kPackedM = 4800;
+
+// Inv entries from the packed M (unit diagonal), tiles of 4x4 (I <= J), k
+// descending from 95 with (fmul, fma) as the reference; stored to slot_of.
+__device__ __forceinline__ void form_packed(const float* M, const float* dinv, float* out, int t, int nThreads) {
+    for (int tile = t; tile < 300; tile += nThreads) {
+        int J = 0, rem = tile;
         while (rem > J) { rem -= J + 1; ++J; }
         const int I = rem;
         float acc[4][4];
@@ -189,10 +232,10 @@ __global__ __launch_bounds__(kFactorThreads) void k_factor_reg(const float* __re
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
-        int k = 95;
-        for (; k >= 4 * J + 3; --k) {
-            const float4 mi = *reinterpret_cast<const float4*>(&A[k * kLda + 4 * I]);
-            const float4 mj = *reinterpret_cast<const float4*>(&A[k * kLda + 4 * J]);
+        for (int k = 95; k >= 4 * J + 3; --k) {
+            const int base = m_row(k);
+            const float4 mi = *reinterpret_cast<const float4*>(&M[base + 4 * I]);
+            const float4 mj = *reinterpret_cast<const float4*>(&M[base + 4 * J]);
             const float d = dinv[k];
             const float fi[4] = {mi.x, mi.y, mi.z, mi.w}, fj[4] = {mj.x, mj.y, mj.z, mj.w};
 #pragma unroll
@@ -201,10 +244,10 @@ __global__ __launch_bounds__(kFactorThreads) void k_factor_reg(const float* __re
                 for (int b = 0; b < 4; ++b) acc[a][b] = __fmaf_rn(d, __fmul_rn(fi[a], fj[b]), acc[a][b]);
         }
 #pragma unroll
-        for (int kk = 2; kk >= 0; --kk) {  // k = 4J + kk: only entries with j = 4J + b <= k
-            k = 4 * J + kk;
-            const float4 mi = *reinterpret_cast<const float4*>(&A[k * kLda + 4 * I]);
-            const float4 mj = *reinterpret_cast<const float4*>(&A[k * kLda + 4 * J]);
+        for (int kk = 2; kk >= 0; --kk) {
+            const int k = 4 * J + kk, base = m_row(k);
+            const float4 mi = *reinterpret_cast<const float4*>(&M[base + 4 * I]);
+            const float4 mj = *reinterpret_cast<const float4*>(&M[base + 4 * J]);
             const float d = dinv[k];
             const float fi[4] = {mi.x, mi.y, mi.z, mi.w}, fj[4] = {mj.x, mj.y, mj.z, mj.w};
 #pragma unroll
@@ -217,17 +260,61 @@ __global__ __launch_bounds__(kFactorThreads) void k_factor_reg(const float* __re
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const int i = 4 * I + a, j = 4 * J + b;
-                if (i < j) A[i * kLda + j] = acc[a][b];
-                else if (i == j) invDiag[i] = acc[a][b];
+                if (i <= j) out[slot_of(i, j)] = acc[a][b];
             }
     }
-    __syncthreads();
-    float* out = inv + blk * kBlockFloats;
-    for (int o = t; o < kBlockFloats; o += kFactorThreads) {
-        const unsigned ij = slotTable[o];
-        const int i = ij & 0xff, j = ij >> 8;
-        out[o] = (i == j) ? invDiag[i] : A[i * kLda + j];
+}
+
+// Register-blocked factor: LDS holds only the pivot row, D^-1 and the packed
+// M (~19.5 KB -> 8 blocks per CU at <= 256 VGPRs), the block is loaded from
+// HBM straight into the lane tiles, and the inverse entries are stored
+// straight to their slots (slot_of) instead of staging the packed output.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_rb(
+    const float* __restrict__ dense, float* __restrict__ inv) {
+    __shared__ __attribute__((aligned(16))) float M[kPackedM];
+    __shared__ __attribute__((aligned(16))) float piv[96];
+    __shared__ float dinv[96];
+    const int t = threadIdx.x;
+    const size_t blk = blockIdx.x;
+    const int rg = t >> 2, cg = t & 3;
+    float v[6][24];
+    {
+        const float* src = dense + blk * kDenseFloats + 24 * cg;
+#pragma unroll
+        for (int m = 0; m < 6; ++m)
+#pragma unroll
+            for (int c4 = 0; c4 < 6; ++c4) {
+                const v4f q = __builtin_nontemporal_load(
+                    reinterpret_cast<const v4f*>(src + (size_t)(rg + 16 * m) * 96 + 4 * c4));
+                v[m][4 * c4] = q.x;
+                v[m][4 * c4 + 1] = q.y;
+                v[m][4 * c4 + 2] = q.z;
+                v[m][4 * c4 + 3] = q.w;
+            }
     }
+    ElimRB<0>::run(v, piv, dinv, rg, cg);
+    // M rows: unit diagonal, L^-1 below, only the stored (padded) columns
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const int k = rg + 16 * m, len = (k & ~3) + 4;
+#pragma unroll
+        for (int c4 = 0; c4 < 6; ++c4) {
+            const int col = 24 * cg + 4 * c4;
+            if (col < len) {
+                float4 q = make_float4(v[m][4 * c4], v[m][4 * c4 + 1], v[m][4 * c4 + 2], v[m][4 * c4 + 3]);
+                if (col == (k & ~3)) {  // the diagonal lies in this float4
+                    const int d = k & 3;
+                    q.x = d == 0 ? 1.f : q.x;
+                    q.y = d == 1 ? 1.f : q.y;
+                    q.z = d == 2 ? 1.f : q.z;
+                    q.w = d == 3 ? 1.f : q.w;
+                }
+                *reinterpret_cast<float4*>(&M[m_row(k) + col]) = q;
+            }
+        }
+    }
+    __syncthreads();
+    form_packed(M, dinv, inv + blk * kBlockFloats, t, 64);
 }
 
 int upload_slot_table(mas_context* h) {
@@ -261,11 +348,14 @@ int copy_block_inverse(mas_context* h, int blk, float* out96) {
 int run_factor(mas_context* h, hipStream_t s) {
     int rc = ensure(h, h->inv, (size_t)h->nBlk * kBlockFloats * 4);
     if (rc) return rc;
-    if (h->factorVariant == 0)
-        k_factor<<<h->nBlk, kFactorThreads, 0, s>>>(P<float>(h->dense), P<unsigned>(h->slotTable), P<float>(h->inv));
-    else
-        k_factor_reg<<<h->nBlk, kFactorThreads, 0, s>>>(P<float>(h->dense), P<unsigned>(h->slotTable),
-                                                         P<float>(h->inv));
+    float* dense = P<float>(h->dense);
+    float* inv = P<float>(h->inv);
+    if (h->factorVariant == 0) {
+        k_factor<<<h->nBlk, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv);
+    } else {
+        k_identity_fix<<<cdiv(h->nBlk * 32, 256), 256, 0, s>>>(dense, h->nBlk * 32);
+        k_factor_rb<<<h->nBlk, 64, 0, s>>>(dense, inv);
+    }
     return hip_check(h, hipGetLastError(), "factor kernel");
 }
 

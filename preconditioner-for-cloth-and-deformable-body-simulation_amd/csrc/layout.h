@@ -62,4 +62,33 @@ __host__ __device__ inline void slot_ij(int o, int& i, int& j) {
     j = r < c ? c : r;
 }
 
+// Inverse of slot_ij: the float offset of Inv entry (i, j) (either order).
+__host__ __device__ inline int slot_of(int i, int j) {
+    int ni = i / 3, nj = j / 3, a = i % 3, b = j % 3;
+    auto at = [](int f, int h, int n) { return ((f >> 2) * 64 + 32 * h + n) * 4 + (f & 3); };
+    if (ni == nj) {  // D(n) upper triangle, half 0, f = 66 + (00 01 02 11 12 22)
+        if (a > b) { const int x = a; a = b; b = x; }
+        const int d = a == 0 ? b : (a == 1 ? 2 + b : 5);
+        return at(66 + d, 0, ni);
+    }
+    int s = (nj - ni) & 31;
+    if (s > 16) {  // stored from the other node: G(m, n) = G(n, m)^T
+        int x = ni; ni = nj; nj = x;
+        x = a; a = b; b = x;
+        s = 32 - s;
+    }
+    if (s == 16) {
+        if (ni >= 16) {  // orient as G(p, p + 16), p < 16
+            int x = ni; ni = nj; nj = x;
+            x = a; a = b; b = x;
+        }
+        if (a == 0) return at(63 + b, 0, ni);
+        if (a == 1) return at(63 + b, 0, ni + 16);
+        return kMainFloats + 3 * ni + b;
+    }
+    const int e = 3 * a + b;
+    if (s <= 7) return at(9 * (s - 1) + e, 0, ni);
+    return at(9 * (s - 8) + e, 1, ni);
+}
+
 }  // namespace mas

@@ -92,7 +92,14 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_OVERLAP")) h->overlap = std::atoi(v);
-    if (hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+    // The side stream gets the highest priority: HIP maps streams onto a few
+    // hardware queues round-robin, and a same-priority side stream can land on
+    // the caller's queue and serialise behind it (measured: MAS_OVERLAP=1 was
+    // slower than serial with a default-priority side stream).
+    int prLeast = 0, prGreatest = 0;
+    hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest);
+    if (const char* v = std::getenv("MAS_SIDE_PRIORITY")) prGreatest = std::atoi(v) ? prGreatest : prLeast;
+    if (hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, prGreatest) != hipSuccess ||
         hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess) {
         mas_destroy(h);

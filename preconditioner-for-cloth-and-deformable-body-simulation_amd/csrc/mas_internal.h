@@ -60,7 +60,7 @@ struct mas_context {
     int overlap = 0;      // 1: coarse chain on stream2 beside the fine blocks (measured slower: 150.8 vs 124.3 us at 1M; env MAS_OVERLAP)
     hipStream_t stream2 = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;
-    int factorVariant = 1;  // 1 = register-resident rows (k_factor_reg); env MAS_FACTOR_VARIANT=0: LDS rows
+    int factorVariant = 2;  // 2 = register-blocked k_factor_rb; env MAS_FACTOR_VARIANT=0: LDS-row k_factor
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     int levelSize[2 * 9] = {};

@@ -46,6 +46,14 @@ def test_facade_header_layouts_compile():
     subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", INC, src], check=True)
 
 
+def test_packed_inverse_slot_layout(tmp_path):
+    """csrc/layout.h: slot_of inverts slot_ij over all 4656 slots (host g++ build)."""
+    src = os.path.join(REPO, "tests", "cpp", "slot_layout_check.cpp")
+    exe = str(tmp_path / "slotchk")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(PKG, "csrc"), src, "-o", exe], check=True)
+    subprocess.run([exe], check=True)
+
+
 def test_no_device_fails_loudly():
     import torch
     if torch.cuda.is_available():

@@ -130,3 +130,22 @@ def test_1m_contacts_parity():
     compare_maps(P, o, mesh.nV)
     r = meshgen.residual(mesh.nV, 0x5EED + 2)
     assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
+
+
+@pytest.mark.parametrize("kind,W,L,nc", [("cloth", 100, 0, 300), ("tet", 16, 3, 0), ("cloth", 33, 0, 0)])
+def test_factor_kernels_agree_bitwise(kind, W, L, nc, monkeypatch):
+    """k_factor (LDS rows, MAS_FACTOR_VARIANT=0) and k_factor_rb (register
+    tiles, default) run the reference's operations in the reference's order:
+    every block inverse (fine and coarse, with padding nodes) must be equal."""
+    from mas_amd import meshgen
+    mesh = cloth(W) if kind == "cloth" else tet(W)
+    contacts = meshgen.vf_contacts(mesh, nc, seed=5) if nc else None
+    monkeypatch.setenv("MAS_FACTOR_VARIANT", "0")
+    P0 = _gpu(mesh, L, contacts=contacts)
+    monkeypatch.setenv("MAS_FACTOR_VARIANT", "2")
+    P2 = _gpu(mesh, L, contacts=contacts)
+    nb = P0.info()["num_blocks"]
+    for blk in range(nb):
+        np.testing.assert_array_equal(P2.block_inverse(blk), P0.block_inverse(blk))
+    r = meshgen.residual(mesh.nV, 17)
+    np.testing.assert_array_equal(P2.Preconditioning(None, r), P0.Preconditioning(None, r))
