@@ -92,10 +92,13 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_OVERLAP")) h->overlap = std::atoi(v);
-    // The side stream gets the highest priority: HIP maps streams onto a few
-    // hardware queues round-robin, and a same-priority side stream can land on
-    // the caller's queue and serialise behind it (measured: MAS_OVERLAP=1 was
-    // slower than serial with a default-priority side stream).
+    // Side stream of the MAS_OVERLAP=1 variant (off by default): highest
+    // priority unless MAS_SIDE_PRIORITY=0.  Streams do run kernels
+    // concurrently on MI355X (scripts/dev/stream_overlap.hip), but the level-2
+    // and level-3 kernels, launched once level 1 is done, wait tens of us for
+    // dispatch slots behind the fine kernel's queued workgroups: 148 vs 124
+    // us per apply with either priority, and CU-masked streams were slower
+    // still (profiles/round1/ab/).
     int prLeast = 0, prGreatest = 0;
     hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest);
     if (const char* v = std::getenv("MAS_SIDE_PRIORITY")) prGreatest = std::atoi(v) ? prGreatest : prLeast;
