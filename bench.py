@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--config", default="1M+contacts", choices=CONFIG_ORDER)
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcg", action="store_true", help="skip the end-to-end PCG solve report")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo only to exercise N>1 on one GPU")
     args = ap.parse_args()
@@ -272,6 +273,28 @@ def main():
         "wall_s_timed": round(wall, 4),
         "cpu_baseline": None,
     }
+
+    if rank == 0 and world == 1 and not args.no_pcg:
+        # end-to-end context (not the metric): one GPU-resident PCG solve of
+        # A x = r with this preconditioner, and the unpreconditioned CG
+        try:
+            dd = torch.from_numpy(np.ascontiguousarray(mesh.diag, np.float32)).cuda()
+            do = torch.from_numpy(np.ascontiguousarray(mesh.off, np.float32)).cuda()
+            dr = torch.from_numpy(np.ascontiguousarray(mesh.starts, np.int32)).cuda()
+            torch.cuda.synchronize()
+            pcg = {}
+            for name, pre in (("mas", True), ("none", False)):
+                x = torch.zeros_like(r)
+                res = P.pcg_solve_device(dd, do, dr, x, r, max_iters=5000, tol=1e-5, precondition=pre,
+                                         stream=sptr)
+                torch.cuda.synchronize()
+                pcg[name] = {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in res.items()}
+                pcg[name]["ms_per_iter"] = round(res["solve_ms"] / max(res["iterations"], 1), 4)
+            pcg["tol"] = 1e-5
+            pcg["note"] = "Prepare excluded; the contact stencils are in the preconditioner only (A = CSR Hessian)"
+            out["pcg_solve"] = pcg
+        except Exception as e:  # context only
+            log(f"pcg report failed: {e!r}")
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

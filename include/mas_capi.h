@@ -124,6 +124,29 @@ int mas_apply(mas_handle h, float* z4, const float* r4);
  * stream: hipStream_t (NULL = handle stream).  Asynchronous. */
 int mas_apply_device(mas_handle h, float* d_z4, const float* d_r4, void* stream);
 
+/* ---- GPU-resident PCG, the caller of the apply ----
+ * Solves A x = b with preconditioned conjugate gradients on the device, A the
+ * Prepare input in the caller's vertex order (diag9[nV], off9[nnz] column-
+ * major 3x3, ranges[nV+1] == nbr_starts, with the neighbour ids given to
+ * mas_allocate), preconditioned by this handle's MAS (precondition = 1) or
+ * not at all (precondition = 0, plain CG).  x: initial guess in, solution out.
+ * Stops when ||r||_2 <= tol ||b||_2 or after max_iters iterations.  Vectors
+ * are [nV][4] fp32 (w written 0); dot products accumulate in fp64 in a fixed
+ * order (deterministic).  The reference has no solver: this is the loop its
+ * callers run around Preconditioning. */
+typedef struct {
+    int iterations;       /* iterations performed */
+    int converged;        /* ||r|| <= tol ||b|| reached */
+    double rel_residual;  /* ||r||_2 / ||b||_2 of the recursively updated residual */
+    double true_rel_residual; /* ||b - A x||_2 / ||b||_2 of the returned x (fp32 vectors: can exceed tol) */
+    double solve_ms;      /* device time from the initial residual to the stop */
+} mas_pcg_result;
+int mas_pcg_solve_device(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges,
+                         float* d_x4, const float* d_b4, int max_iters, float tol, int precondition,
+                         mas_pcg_result* out, void* stream);
+/* The same with host arrays (copied in and out; synchronous). */
+int mas_pcg_solve(mas_handle h, const float* diag9, const float* off9, const int* ranges, float* x4,
+                  const float* b4, int max_iters, float tol, int precondition, mas_pcg_result* out);
 /* Record HIP events around the apply kernels of every mas_apply_device call
  * (up to 4096 applies) and reset the averages in mas_stats. */
 int mas_set_profiling(mas_handle h, int enable);

@@ -198,6 +198,48 @@ int mas_apply_device(mas_handle h, float* d_z4, const float* d_r4, void* stream)
     return run_apply(h, reinterpret_cast<float4*>(d_z4), reinterpret_cast<const float4*>(d_r4), s);
 }
 
+int mas_pcg_solve_device(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges, float* d_x4,
+                         const float* d_b4, int max_iters, float tol, int precondition, mas_pcg_result* out,
+                         void* stream) {
+    if (!h) return MAS_ERR_ARG;
+    if (!d_diag9 || !d_off9 || !d_ranges || !d_x4 || !d_b4)
+        return fail(h, MAS_ERR_ARG, "mas_pcg_solve_device: null pointer");
+    if ((reinterpret_cast<uintptr_t>(d_x4) | reinterpret_cast<uintptr_t>(d_b4)) & 15)
+        return fail(h, MAS_ERR_ARG, "mas_pcg_solve_device: vectors must be 16-byte aligned");
+    if (max_iters < 0 || !(tol >= 0.0f)) return fail(h, MAS_ERR_ARG, "mas_pcg_solve_device: bad max_iters / tol");
+    if (precondition && !h->prepared) return fail(h, MAS_ERR_STATE, "preconditioned solve before prepare");
+    if (!h->allocated) return fail(h, MAS_ERR_STATE, "solve before allocate");
+    hipSetDevice(h->device);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    return run_pcg(h, d_diag9, d_off9, d_ranges, reinterpret_cast<float4*>(d_x4),
+                   reinterpret_cast<const float4*>(d_b4), max_iters, tol, precondition, out, s);
+}
+
+int mas_pcg_solve(mas_handle h, const float* diag9, const float* off9, const int* ranges, float* x4, const float* b4,
+                  int max_iters, float tol, int precondition, mas_pcg_result* out) {
+    if (!h) return MAS_ERR_ARG;
+    if (!diag9 || !off9 || !ranges || !x4 || !b4) return fail(h, MAS_ERR_ARG, "mas_pcg_solve: null pointer");
+    if (!h->allocated) return fail(h, MAS_ERR_STATE, "solve before allocate");
+    hipSetDevice(h->device);
+    const size_t nV = h->nV, nnz = h->nnz, vb = nV * 16;
+    MAS_TRY(ensure(h, h->diagStage, nV * 36));
+    MAS_TRY(ensure(h, h->offStage, nnz * 36));
+    MAS_TRY(ensure(h, h->rangeStage, (nV + 1) * 4));
+    MAS_TRY(ensure(h, h->pcgStage, 2 * vb));
+    float* dx = P<float>(h->pcgStage);
+    float* db = dx + 4 * nV;
+    MAS_TRY(hip_check(h, hipMemcpyAsync(h->diagStage.p, diag9, nV * 36, hipMemcpyHostToDevice, h->stream), "H2D diag"));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(h->offStage.p, off9, nnz * 36, hipMemcpyHostToDevice, h->stream), "H2D off"));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(h->rangeStage.p, ranges, (nV + 1) * 4, hipMemcpyHostToDevice, h->stream),
+                      "H2D ranges"));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(dx, x4, vb, hipMemcpyHostToDevice, h->stream), "H2D x"));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(db, b4, vb, hipMemcpyHostToDevice, h->stream), "H2D b"));
+    MAS_TRY(mas_pcg_solve_device(h, P<float>(h->diagStage), P<float>(h->offStage), P<int>(h->rangeStage), dx, db,
+                                 max_iters, tol, precondition, out, h->stream));
+    MAS_TRY(hip_check(h, hipMemcpyAsync(x4, dx, vb, hipMemcpyDeviceToHost, h->stream), "D2H x"));
+    return hip_check(h, hipStreamSynchronize(h->stream), "solve sync");
+}
+
 int mas_apply(mas_handle h, float* z4, const float* r4) {
     if (!h) return MAS_ERR_ARG;
     if (!z4 || !r4) return fail(h, MAS_ERR_ARG, "mas_apply: null vector");

@@ -78,6 +78,7 @@ struct mas_context {
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff;
+    mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     std::vector<int> l1First;  // first level-1 local id per level-0 bank (+ n1), for sharding
     int shardWorld = 0;
     // staging for host-pointer entry points
@@ -98,7 +99,7 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -133,5 +134,7 @@ int upload_slot_table(mas_context* h);
 int prepare_apply_tables(mas_context* h, hipStream_t s);
 int compute_l1_first(mas_context* h, hipStream_t s);
 int copy_block_inverse(mas_context* h, int blk, float* out96);
+int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,
+            const float4* d_b, int maxIters, float tol, int precondition, mas_pcg_result* res, hipStream_t s);
 
 }  // namespace mas

@@ -32,7 +32,8 @@ STATUS = {0: "MAS_OK", -1: "MAS_ERR_ARG", -2: "MAS_ERR_HIP", -3: "MAS_ERR_CAPACI
 EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_allocate", "mas_prepare",
            "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_get_info",
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
-           "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish"]
+           "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
+           "mas_pcg_solve_device", "mas_pcg_solve"]
 
 
 class mas_config(ctypes.Structure):
@@ -58,6 +59,14 @@ class mas_stats(ctypes.Structure):
 class mas_shard(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("rank", "world", "fine_block_begin", "fine_block_end", "vert_begin",
                                             "vert_end", "l1_begin", "l1_end", "seg_max")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class mas_pcg_result(ctypes.Structure):
+    _fields_ = [("iterations", ctypes.c_int), ("converged", ctypes.c_int), ("rel_residual", ctypes.c_double),
+                ("true_rel_residual", ctypes.c_double), ("solve_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -106,6 +115,9 @@ def lib():
         L.mas_shard_setup.argtypes = [P, I, I, ctypes.POINTER(mas_shard)]
         L.mas_apply_shard_restrict.argtypes = [P, I, I, P, P, P]
         L.mas_apply_shard_finish.argtypes = [P, I, I, P, P, P, P]
+        F = ctypes.c_float
+        L.mas_pcg_solve_device.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result), P]
+        L.mas_pcg_solve.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result)]
         _lib = L
     return _lib
 
@@ -206,6 +218,29 @@ class SeSchwarzPreconditioner:
     def shard_finish(self, rank, world, gathered, r, z, stream=None):
         self._check(self._L.mas_apply_shard_finish(self.h, rank, world, _ptr(gathered), _ptr(r), _ptr(z),
                                                    _ptr(stream)), "shard_finish")
+
+    # ---- GPU-resident PCG (include/mas_capi.h) ----
+    def pcg_solve(self, diagonal, csrOffDiagonals, csrRanges, b, x0=None, max_iters=1000, tol=1e-5,
+                  precondition=True):
+        """Host arrays: returns (x [nV,4] float32, result dict)."""
+        d = _c(diagonal, np.float32)
+        o = _c(csrOffDiagonals, np.float32)
+        r = _c(csrRanges, np.int32)
+        bb = _c(b, np.float32)
+        x = np.zeros_like(bb) if x0 is None else np.array(x0, dtype=np.float32, copy=True)
+        res = mas_pcg_result()
+        self._check(self._L.mas_pcg_solve(self.h, _ptr(d), _ptr(o), _ptr(r), _ptr(x), _ptr(bb), int(max_iters),
+                                          float(tol), int(bool(precondition)), ctypes.byref(res)), "pcg_solve")
+        return x, res.as_dict()
+
+    def pcg_solve_device(self, d_diag, d_off, d_ranges, x, b, max_iters=1000, tol=1e-5, precondition=True,
+                         stream=None) -> dict:
+        """Device arrays (torch cuda tensors or raw pointers); x is updated in place."""
+        res = mas_pcg_result()
+        self._check(self._L.mas_pcg_solve_device(self.h, _ptr(d_diag), _ptr(d_off), _ptr(d_ranges), _ptr(x),
+                                                 _ptr(b), int(max_iters), float(tol), int(bool(precondition)),
+                                                 ctypes.byref(res), _ptr(stream)), "pcg_solve_device")
+        return res.as_dict()
 
     # ---- introspection ----
     def set_profiling(self, on: bool):
