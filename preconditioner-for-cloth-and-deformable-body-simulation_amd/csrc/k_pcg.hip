@@ -13,11 +13,19 @@
 // off9[nnz] (3x3 column-major, SeMatrix.h:650-682) with the neighbour CSR
 // (ranges == nbr_starts, nbr_idx from Allocate).  Vectors are float4[nV]
 // (SeVec3fSimd).  Vector arithmetic is fp32; every dot product accumulates in
-// fp64 over a fixed grid and is finished by one workgroup in a fixed order, so
-// a solve is run-to-run deterministic.  The scalars (alpha, beta, |r|^2, the
-// stop flag) live in device memory: the host enqueues iterations in chunks
-// and reads the state once per chunk; every kernel of a finished solve exits
-// at its first instruction.
+// fp64 over a fixed grid of workgroups; the kernel that consumes a dot
+// product sums the per-workgroup partials itself, in the same fixed order in
+// every workgroup (no single-workgroup "finish" launches), so a solve is
+// run-to-run deterministic.  The scalars (rz, |r|^2, the stop flag) live in
+// device memory: the host enqueues iterations in chunks and reads the state
+// once per chunk; every kernel of a finished solve exits at its first
+// instruction.
+//
+// SpMV: G lanes per row (G = 8 for the cloth valence, 16/32 above), lane j
+// takes the row's neighbours j, j+G, ...: the 36-byte blocks of consecutive
+// rows are contiguous in the CSR, so one wave-instruction reads ~64
+// consecutive blocks; the G partial products are combined by a fixed xor
+// butterfly.  Per iteration: spmv, update_xr, apply (or copy), rz, update_p.
 #include "mas_internal.h"
 
 namespace mas {
@@ -26,9 +34,13 @@ constexpr int kPcgThreads = 256;
 constexpr int kPcgBlocks = 1024;  // fixed grid: partial sums in a fixed order
 
 struct PcgState {
-    double rz, pAp, rr, bb, alpha, beta, tol2, rrTrue;
+    double rz[2];  // r.z of the current / next iteration (slot it & 1)
+    double rr, bb, alpha, tol2, rrTrue;
     int done, iters, maxIters, pad;
 };
+
+// partial-sum slots (kPcgBlocks doubles each)
+enum { kPartPAp = 0, kPartRR = 1, kPartRZ = 2, kPartBB = 3, kParts = 4 };
 
 __device__ __forceinline__ float3 mat3_mul(const float* __restrict__ m, float4 x) {
     // column-major 3x3: y_i = sum_j m[3 j + i] x_j
@@ -37,17 +49,30 @@ __device__ __forceinline__ float3 mat3_mul(const float* __restrict__ m, float4 x
                        __fadd_rn(__fadd_rn(__fmul_rn(m[2], x.x), __fmul_rn(m[5], x.y)), __fmul_rn(m[8], x.z)));
 }
 
-// y = A x for vertex v (diagonal first, then the neighbours in CSR order)
-__device__ __forceinline__ float3 spmv_row(int v, const int* __restrict__ starts, const int* __restrict__ idx,
-                                           const float* __restrict__ diag, const float* __restrict__ off,
-                                           const float4* __restrict__ x) {
-    float3 acc = mat3_mul(diag + 9 * (size_t)v, x[v]);
-    const int e0 = starts[v], e1 = starts[v + 1];
-    for (int e = e0; e < e1; ++e) {
-        const float3 t = mat3_mul(off + 9 * (size_t)e, x[idx[e]]);
-        acc.x = __fadd_rn(acc.x, t.x);
-        acc.y = __fadd_rn(acc.y, t.y);
-        acc.z = __fadd_rn(acc.z, t.z);
+__device__ __forceinline__ void add3(float3& a, float3 b) {
+    a.x = __fadd_rn(a.x, b.x);
+    a.y = __fadd_rn(a.y, b.y);
+    a.z = __fadd_rn(a.z, b.z);
+}
+
+// (A x)[v] for the G-lane group of row v; the full sum is returned in every lane
+// of the group.  Lane j: neighbours j, j+G, ... in CSR order, lane 0 adds the
+// diagonal first; then a fixed xor butterfly over the group.
+template <int G>
+__device__ __forceinline__ float3 spmv_group(int v, bool valid, int sub, const int* __restrict__ starts,
+                                             const int* __restrict__ idx, const float* __restrict__ diag,
+                                             const float* __restrict__ off, const float4* __restrict__ x) {
+    float3 acc = make_float3(0.f, 0.f, 0.f);
+    if (valid) {
+        if (sub == 0) acc = mat3_mul(diag + 9 * (size_t)v, x[v]);
+        const int e1 = starts[v + 1];
+        for (int e = starts[v] + sub; e < e1; e += G) add3(acc, mat3_mul(off + 9 * (size_t)e, x[idx[e]]));
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+        acc.x = __fadd_rn(acc.x, __shfl_xor(acc.x, o));
+        acc.y = __fadd_rn(acc.y, __shfl_xor(acc.y, o));
+        acc.z = __fadd_rn(acc.z, __shfl_xor(acc.z, o));
     }
     return acc;
 }
@@ -56,74 +81,68 @@ __device__ __forceinline__ double dot3(float3 a, float4 b) {
     return (double)a.x * b.x + (double)a.y * b.y + (double)a.z * b.z;
 }
 
-// block sum of up to two doubles -> partial[2 * blockIdx.x + {0, 1}]
-__device__ __forceinline__ void block_partials(double a, double b, double* __restrict__ partial) {
-    __shared__ double sa[kPcgThreads / 64], sb[kPcgThreads / 64];
-    for (int o = 32; o > 0; o >>= 1) {
-        a += __shfl_xor(a, o);
-        b += __shfl_xor(b, o);
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        sa[w] = a;
-        sb[w] = b;
-    }
+// workgroup sum of one double per thread -> partial[blockIdx.x] (fixed order)
+__device__ __forceinline__ void block_partial(double a, double* __restrict__ partial) {
+    __shared__ double sa[kPcgThreads / 64];
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    if ((threadIdx.x & 63) == 0) sa[threadIdx.x >> 6] = a;
     __syncthreads();
     if (threadIdx.x == 0) {
-        double ta = 0.0, tb = 0.0;
-        for (int i = 0; i < kPcgThreads / 64; ++i) {
-            ta += sa[i];
-            tb += sb[i];
-        }
-        partial[2 * blockIdx.x] = ta;
-        partial[2 * blockIdx.x + 1] = tb;
+        double t = 0.0;
+        for (int i = 0; i < kPcgThreads / 64; ++i) t += sa[i];
+        partial[blockIdx.x] = t;
     }
 }
 
-// one workgroup: fixed-order sums of the kPcgBlocks partial pairs
-__device__ __forceinline__ void finish_sums(const double* __restrict__ partial, double& a, double& b) {
-    __shared__ double sa[kPcgThreads], sb[kPcgThreads];
-    double ta = 0.0, tb = 0.0;
-    for (int i = threadIdx.x; i < kPcgBlocks; i += kPcgThreads) {
-        ta += partial[2 * i];
-        tb += partial[2 * i + 1];
-    }
-    sa[threadIdx.x] = ta;
-    sb[threadIdx.x] = tb;
+// every workgroup: the same fixed-order sum of the kPcgBlocks partials
+__device__ __forceinline__ double sum_partials(const double* __restrict__ partial) {
+    __shared__ double sa[kPcgThreads];
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < kPcgBlocks / kPcgThreads; ++i) t += partial[threadIdx.x + i * kPcgThreads];
+    sa[threadIdx.x] = t;
     __syncthreads();
     for (int s = kPcgThreads / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            sa[threadIdx.x] += sa[threadIdx.x + s];
-            sb[threadIdx.x] += sb[threadIdx.x + s];
-        }
+        if (threadIdx.x < s) sa[threadIdx.x] += sa[threadIdx.x + s];
         __syncthreads();
     }
-    a = sa[0];
-    b = sb[0];
+    return sa[0];
 }
 
-// r = b - A x; partials (r.r, b.b)
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_init(int nV, const int* __restrict__ starts,
-                                                          const int* __restrict__ idx, const float* __restrict__ diag,
-                                                          const float* __restrict__ off, const float4* __restrict__ x,
-                                                          const float4* __restrict__ b, float4* __restrict__ r,
-                                                          double* __restrict__ partial) {
+// r = b - A x; partials r.r (kPartRR) and b.b (kPartBB).  Also the final
+// true-residual pass (r = scratch).
+template <int G>
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_residual(int nV, const int* __restrict__ starts,
+                                                              const int* __restrict__ idx,
+                                                              const float* __restrict__ diag,
+                                                              const float* __restrict__ off,
+                                                              const float4* __restrict__ x,
+                                                              const float4* __restrict__ b, float4* __restrict__ r,
+                                                              double* __restrict__ part) {
+    const int lane = threadIdx.x & 63, sub = lane % G;
+    const int wave = blockIdx.x * (kPcgThreads / 64) + (threadIdx.x >> 6);
     double rr = 0.0, bb = 0.0;
-    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
-        const float3 ax = spmv_row(v, starts, idx, diag, off, x);
-        const float4 bv = b[v];
-        const float4 rv = make_float4(__fsub_rn(bv.x, ax.x), __fsub_rn(bv.y, ax.y), __fsub_rn(bv.z, ax.z), 0.f);
-        r[v] = rv;
-        rr += dot3(make_float3(rv.x, rv.y, rv.z), rv);
-        bb += dot3(make_float3(bv.x, bv.y, bv.z), bv);
+    for (int base = wave * (64 / G); base < nV; base += kPcgBlocks * (kPcgThreads / 64) * (64 / G)) {
+        const int v = base + lane / G;
+        const float3 ax = spmv_group<G>(v, v < nV, sub, starts, idx, diag, off, x);
+        if (sub == 0 && v < nV) {
+            const float4 bv = b[v];
+            const float4 rv = make_float4(__fsub_rn(bv.x, ax.x), __fsub_rn(bv.y, ax.y), __fsub_rn(bv.z, ax.z), 0.f);
+            r[v] = rv;
+            rr += dot3(make_float3(rv.x, rv.y, rv.z), rv);
+            bb += dot3(make_float3(bv.x, bv.y, bv.z), bv);
+        }
     }
-    block_partials(rr, bb, partial);
+    block_partial(rr, part + kPartRR * kPcgBlocks);
+    block_partial(bb, part + kPartBB * kPcgBlocks);
 }
 
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_init_finish(const double* __restrict__ partial,
-                                                                 PcgState* __restrict__ st) {
-    double rr, bb;
-    finish_sums(partial, rr, bb);
+// 0 iterations done yet: stop at once if |r0| <= tol |b| (or max_iters == 0)
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_start(const double* __restrict__ part,
+                                                           PcgState* __restrict__ st) {
+    const double rr = sum_partials(part + kPartRR * kPcgBlocks);
+    const double bb = sum_partials(part + kPartBB * kPcgBlocks);
     if (threadIdx.x == 0) {
         st->rr = rr;
         st->bb = bb;
@@ -132,88 +151,44 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_init_finish(const double* _
     }
 }
 
-// after the loop: |b - A x|^2 (into the spare Ap vector)
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_true_finish(const double* __restrict__ partial,
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_true_finish(const double* __restrict__ part,
                                                                  PcgState* __restrict__ st) {
-    double rr, bb;
-    finish_sums(partial, rr, bb);
+    const double rr = sum_partials(part + kPartRR * kPcgBlocks);
     if (threadIdx.x == 0) st->rrTrue = rr;
 }
 
-// partials (r.z, 0); also p = z on the first call (copy_p)
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_rz(int nV, const float4* __restrict__ r,
-                                                        const float4* __restrict__ z, float4* __restrict__ p,
-                                                        int copy_p, const PcgState* __restrict__ st,
-                                                        double* __restrict__ partial) {
-    if (st->done) return;
-    double rz = 0.0;
-    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
-        const float4 zv = z[v];
-        rz += dot3(make_float3(zv.x, zv.y, zv.z), r[v]);
-        if (copy_p) p[v] = zv;
-    }
-    block_partials(rz, 0.0, partial);
-}
-
-// first: rz = r.z; later: beta = r.z / rz, rz = r.z
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_rz_finish(const double* __restrict__ partial, int first,
-                                                               PcgState* __restrict__ st) {
-    if (st->done) return;
-    double rz, unused;
-    finish_sums(partial, rz, unused);
-    if (threadIdx.x == 0) {
-        st->beta = first ? 0.0 : rz / st->rz;
-        st->rz = rz;
-    }
-}
-
-// p = z + beta p
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_update_p(int nV, const float4* __restrict__ z,
-                                                              float4* __restrict__ p,
-                                                              const PcgState* __restrict__ st) {
-    if (st->done) return;
-    const float beta = (float)st->beta;
-    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
-        const float4 zv = z[v], pv = p[v];
-        p[v] = make_float4(__fmaf_rn(beta, pv.x, zv.x), __fmaf_rn(beta, pv.y, zv.y), __fmaf_rn(beta, pv.z, zv.z), 0.f);
-    }
-}
-
-// Ap = A p; partials (p.Ap, 0)
+// Ap = A p; partials p.Ap
+template <int G>
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __restrict__ starts,
                                                           const int* __restrict__ idx, const float* __restrict__ diag,
                                                           const float* __restrict__ off, const float4* __restrict__ p,
                                                           float4* __restrict__ ap, const PcgState* __restrict__ st,
-                                                          double* __restrict__ partial) {
+                                                          double* __restrict__ part) {
     if (st->done) return;
+    const int lane = threadIdx.x & 63, sub = lane % G;
+    const int wave = blockIdx.x * (kPcgThreads / 64) + (threadIdx.x >> 6);
     double pap = 0.0;
-    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
-        const float3 y = spmv_row(v, starts, idx, diag, off, p);
-        ap[v] = make_float4(y.x, y.y, y.z, 0.f);
-        pap += dot3(y, p[v]);
+    for (int base = wave * (64 / G); base < nV; base += kPcgBlocks * (kPcgThreads / 64) * (64 / G)) {
+        const int v = base + lane / G;
+        const float3 y = spmv_group<G>(v, v < nV, sub, starts, idx, diag, off, p);
+        if (sub == 0 && v < nV) {
+            ap[v] = make_float4(y.x, y.y, y.z, 0.f);
+            pap += dot3(y, p[v]);
+        }
     }
-    block_partials(pap, 0.0, partial);
+    block_partial(pap, part + kPartPAp * kPcgBlocks);
 }
 
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_alpha(const double* __restrict__ partial,
-                                                           PcgState* __restrict__ st) {
-    if (st->done) return;
-    double pap, unused;
-    finish_sums(partial, pap, unused);
-    if (threadIdx.x == 0) {
-        st->pAp = pap;
-        st->alpha = st->rz / pap;
-    }
-}
-
-// x += alpha p; r -= alpha Ap; partials (r.r, 0)
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_update_xr(int nV, const float4* __restrict__ p,
+// alpha = rz / p.Ap; x += alpha p; r -= alpha Ap; partials r.r
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_update_xr(int nV, int it, const float4* __restrict__ p,
                                                                const float4* __restrict__ ap, float4* __restrict__ x,
-                                                               float4* __restrict__ r,
-                                                               const PcgState* __restrict__ st,
-                                                               double* __restrict__ partial) {
+                                                               float4* __restrict__ r, PcgState* __restrict__ st,
+                                                               double* __restrict__ part) {
     if (st->done) return;
-    const float alpha = (float)st->alpha;
+    const double pap = sum_partials(part + kPartPAp * kPcgBlocks);
+    const double alphaD = st->rz[it & 1] / pap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->alpha = alphaD;
+    const float alpha = (float)alphaD;
     double rr = 0.0;
     for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
         const float4 pv = p[v], av = ap[v], xv = x[v], rv = r[v];
@@ -224,18 +199,53 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update_xr(int nV, const flo
         r[v] = rn;
         rr += dot3(make_float3(rn.x, rn.y, rn.z), rn);
     }
-    block_partials(rr, 0.0, partial);
+    block_partial(rr, part + kPartRR * kPcgBlocks);
 }
 
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_check(const double* __restrict__ partial,
-                                                           PcgState* __restrict__ st) {
+// it >= 0: after iteration it, stop if |r| <= tol |b| or it + 1 == max_iters
+// (workgroup 0 records it); otherwise partials r.z.
+// it < 0 (start): partials r.z and p = z.
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_rz(int nV, int it, const float4* __restrict__ r,
+                                                        const float4* __restrict__ z, float4* __restrict__ p,
+                                                        PcgState* __restrict__ st, double* __restrict__ part) {
     if (st->done) return;
-    double rr, unused;
-    finish_sums(partial, rr, unused);
-    if (threadIdx.x == 0) {
-        st->rr = rr;
-        st->iters += 1;
-        st->done = (rr <= st->tol2 * st->bb) || st->iters >= st->maxIters;
+    if (it >= 0) {
+        const double rr = sum_partials(part + kPartRR * kPcgBlocks);
+        const bool stop = (rr <= st->tol2 * st->bb) || it + 1 >= st->maxIters;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->rr = rr;
+            st->iters = it + 1;
+            if (stop) st->done = 1;
+        }
+        if (stop) return;  // the same decision in every workgroup
+    }
+    double rz = 0.0;
+    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
+        const float4 zv = z[v];
+        rz += dot3(make_float3(zv.x, zv.y, zv.z), r[v]);
+        if (it < 0) p[v] = zv;
+    }
+    block_partial(rz, part + kPartRZ * kPcgBlocks);
+}
+
+// start: rz[0] = r.z
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_rz0(PcgState* __restrict__ st, const double* __restrict__ part) {
+    if (st->done) return;
+    const double rz = sum_partials(part + kPartRZ * kPcgBlocks);
+    if (threadIdx.x == 0) st->rz[0] = rz;
+}
+
+// beta = r.z (new) / r.z (old); p = z + beta p; workgroup 0 stores the new r.z
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_update_p(int nV, int it, const float4* __restrict__ z,
+                                                              float4* __restrict__ p, PcgState* __restrict__ st,
+                                                              const double* __restrict__ part) {
+    if (st->done) return;
+    const double rzNew = sum_partials(part + kPartRZ * kPcgBlocks);
+    const float beta = (float)(rzNew / st->rz[it & 1]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->rz[(it + 1) & 1] = rzNew;
+    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
+        const float4 zv = z[v], pv = p[v];
+        p[v] = make_float4(__fmaf_rn(beta, pv.x, zv.x), __fmaf_rn(beta, pv.y, zv.y), __fmaf_rn(beta, pv.z, zv.z), 0.f);
     }
 }
 
@@ -245,21 +255,62 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_copy(int nV, const float4* 
     for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) dst[v] = src[v];
 }
 
-int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,
-            const float4* d_b, int maxIters, float tol, int precondition, mas_pcg_result* res, hipStream_t s) {
+template <int G>
+static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,
+                    const float4* d_b, int maxIters, int precondition, PcgState& host, PcgState* st, hipStream_t s,
+                    hipEvent_t e1) {
     const int nV = h->nV;
-    int rc;
-    if ((rc = ensure(h, h->pcgVec, (size_t)nV * 16 * 4)) ||
-        (rc = ensure(h, h->pcgPartial, (size_t)kPcgBlocks * 2 * sizeof(double))) ||
-        (rc = ensure(h, h->pcgState, sizeof(PcgState))))
-        return rc;
     float4* r = P<float4>(h->pcgVec);
     float4* z = r + nV;
     float4* p = z + nV;
     float4* ap = p + nV;
     double* part = P<double>(h->pcgPartial);
-    PcgState* st = P<PcgState>(h->pcgState);
     const int* idx = P<int>(h->idx);
+    const dim3 g(kPcgBlocks), b(kPcgThreads);
+    int rc;
+    k_pcg_residual<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, r, part);
+    k_pcg_start<<<1, b, 0, s>>>(part, st);
+    if (precondition) {
+        if ((rc = run_apply(h, z, r, s))) return rc;
+    } else {
+        k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st);
+    }
+    k_pcg_rz<<<g, b, 0, s>>>(nV, -1, r, z, p, st, part);
+    k_pcg_rz0<<<1, b, 0, s>>>(st, part);
+    const int chunk = 4;
+    for (int it = 0; it < maxIters; it += chunk) {
+        for (int k = it; k < it + chunk && k < maxIters; ++k) {
+            k_pcg_spmv<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, p, ap, st, part);
+            k_pcg_update_xr<<<g, b, 0, s>>>(nV, k, p, ap, d_x, r, st, part);
+            if (precondition) {
+                if ((rc = run_apply(h, z, r, s))) return rc;
+            } else {
+                k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st);
+            }
+            k_pcg_rz<<<g, b, 0, s>>>(nV, k, r, z, p, st, part);
+            k_pcg_update_p<<<g, b, 0, s>>>(nV, k, z, p, st, part);
+        }
+        if ((rc = hip_check(h, hipMemcpyAsync(&host, st, sizeof(host), hipMemcpyDeviceToHost, s), "D2H pcg state")) ||
+            (rc = hip_check(h, hipStreamSynchronize(s), "pcg sync")))
+            return rc;
+        if (host.done) break;
+    }
+    hipEventRecord(e1, s);
+    // the true residual of the returned x (the fp32 recursion drifts from it)
+    k_pcg_residual<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, ap, part);
+    k_pcg_true_finish<<<1, b, 0, s>>>(part, st);
+    return MAS_OK;
+}
+
+int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,
+            const float4* d_b, int maxIters, float tol, int precondition, mas_pcg_result* res, hipStream_t s) {
+    const int nV = h->nV;
+    int rc;
+    if ((rc = ensure(h, h->pcgVec, (size_t)nV * 16 * 4)) ||
+        (rc = ensure(h, h->pcgPartial, (size_t)kPcgBlocks * kParts * sizeof(double))) ||
+        (rc = ensure(h, h->pcgState, sizeof(PcgState))))
+        return rc;
+    PcgState* st = P<PcgState>(h->pcgState);
     PcgState init{};
     init.tol2 = (double)tol * (double)tol;
     init.maxIters = maxIters;
@@ -269,42 +320,15 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
     hipEventRecord(e0, s);
     if ((rc = hip_check(h, hipMemcpyAsync(st, &init, sizeof(init), hipMemcpyHostToDevice, s), "H2D pcg state")))
         return rc;
-    const dim3 g(kPcgBlocks), b(kPcgThreads);
-    k_pcg_init<<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, r, part);
-    k_pcg_init_finish<<<1, b, 0, s>>>(part, st);
-    if (precondition) {
-        if ((rc = run_apply(h, z, r, s))) return rc;
-    } else {
-        k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st);
-    }
-    k_pcg_rz<<<g, b, 0, s>>>(nV, r, z, p, 1, st, part);
-    k_pcg_rz_finish<<<1, b, 0, s>>>(part, 1, st);
     PcgState host{};
-    const int chunk = 4;
-    for (int it = 0; it < maxIters; it += chunk) {
-        for (int k = 0; k < chunk && it + k < maxIters; ++k) {
-            k_pcg_spmv<<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, p, ap, st, part);
-            k_pcg_alpha<<<1, b, 0, s>>>(part, st);
-            k_pcg_update_xr<<<g, b, 0, s>>>(nV, p, ap, d_x, r, st, part);
-            k_pcg_check<<<1, b, 0, s>>>(part, st);
-            if (precondition) {
-                if ((rc = run_apply(h, z, r, s))) return rc;
-            } else {
-                k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st);
-            }
-            k_pcg_rz<<<g, b, 0, s>>>(nV, r, z, p, 0, st, part);
-            k_pcg_rz_finish<<<1, b, 0, s>>>(part, 0, st);
-            k_pcg_update_p<<<g, b, 0, s>>>(nV, z, p, st);
-        }
-        if ((rc = hip_check(h, hipMemcpyAsync(&host, st, sizeof(host), hipMemcpyDeviceToHost, s), "D2H pcg state")) ||
-            (rc = hip_check(h, hipStreamSynchronize(s), "pcg sync")))
-            return rc;
-        if (host.done) break;
-    }
-    hipEventRecord(e1, s);
-    // the true residual of the returned x (fp32 recursion drifts from it)
-    k_pcg_init<<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, ap, part);
-    k_pcg_true_finish<<<1, b, 0, s>>>(part, st);
+    const int valence = h->maxNbr - 1;  // max neighbours per row (maxNbr counts the vertex itself)
+    if (valence <= 8)
+        rc = pcg_loop<8>(h, d_diag9, d_off9, d_ranges, d_x, d_b, maxIters, precondition, host, st, s, e1);
+    else if (valence <= 16)
+        rc = pcg_loop<16>(h, d_diag9, d_off9, d_ranges, d_x, d_b, maxIters, precondition, host, st, s, e1);
+    else
+        rc = pcg_loop<32>(h, d_diag9, d_off9, d_ranges, d_x, d_b, maxIters, precondition, host, st, s, e1);
+    if (rc) return rc;
     if ((rc = hip_check(h, hipMemcpyAsync(&host, st, sizeof(host), hipMemcpyDeviceToHost, s), "D2H pcg state")) ||
         (rc = hip_check(h, hipStreamSynchronize(s), "pcg sync")))
         return rc;
