@@ -191,6 +191,41 @@ def vf_contacts(mesh: Mesh, count: int, seed: int = 3, bary=(0.25, 0.25), stiff:
     return vf, counts
 
 
+def ef_contacts(mesh: Mesh, count: int, seed: int = 5, bary=(0.3, 0.2, 0.25), stiff: float = 50.0):
+    """Edge-face contact records (EfSet, SeCollisionElements.h:33-41): e = rng() % nE,
+    f = rng() % nF, fixed barycentrics, unit normal (0.6, 0, 0.8).  Counts [nE+1],
+    total at [nE] (.cpp:306)."""
+    raw = _mt_raw(seed, 2 * count).astype(np.uint64)
+    ef = np.zeros(count, dtype=EF_DTYPE)
+    ef["eId"] = (raw[0::2] % np.uint64(mesh.edges.shape[0])).astype(np.int32)
+    ef["fId"] = (raw[1::2] % np.uint64(mesh.faces.shape[0])).astype(np.int32)
+    ef["stiff"] = stiff
+    for k in range(3):
+        ef["bary"][:, k] = bary[k]
+    ef["normal"][:, 0] = 0.6
+    ef["normal"][:, 2] = 0.8
+    counts = np.zeros(mesh.edges.shape[0] + 1, dtype=np.uint32)
+    counts[-1] = count
+    return ef, counts
+
+
+def ee_contacts(mesh: Mesh, count: int, seed: int = 7, bary=(0.4, 0.7), stiff: float = 80.0):
+    """Edge-edge contact records (EeSet, SeCollisionElements.h:43-50): two edges
+    rng() % nE, fixed barycentrics, unit normal (0, 0.6, 0.8).  Counts [nE+1]."""
+    raw = _mt_raw(seed, 2 * count).astype(np.uint64)
+    ee = np.zeros(count, dtype=EE_DTYPE)
+    ee["eId0"] = (raw[0::2] % np.uint64(mesh.edges.shape[0])).astype(np.int32)
+    ee["eId1"] = (raw[1::2] % np.uint64(mesh.edges.shape[0])).astype(np.int32)
+    ee["stiff"] = stiff
+    ee["bary"][:, 0] = bary[0]
+    ee["bary"][:, 1] = bary[1]
+    ee["normal"][:, 1] = 0.6
+    ee["normal"][:, 2] = 0.8
+    counts = np.zeros(mesh.edges.shape[0] + 1, dtype=np.uint32)
+    counts[-1] = count
+    return ee, counts
+
+
 def residual(nV: int, seed: int) -> np.ndarray:
     """r ~ U(-1, 1)^3, w = 0 (float32)."""
     rng = np.random.default_rng(seed)

@@ -149,3 +149,49 @@ def test_factor_kernels_agree_bitwise(kind, W, L, nc, monkeypatch):
         np.testing.assert_array_equal(P2.block_inverse(blk), P0.block_inverse(blk))
     r = meshgen.residual(mesh.nV, 17)
     np.testing.assert_array_equal(P2.Preconditioning(None, r), P0.Preconditioning(None, r))
+
+
+@pytest.mark.parametrize("W,L,n", [(64, 0, 300), (100, 3, 1000)])
+def test_all_contact_types_parity(W, L, n):
+    """EF + EE + VF stencils together (B-3 set offsets fixed on both sides):
+    maps bit-exact, stencil count equal, assembled blocks within fp32-atomic
+    reordering, z within the north-star tolerance."""
+    import mas_amd
+    from mas_amd import meshgen
+    from oracle import Oracle
+    mesh = cloth(W)
+    ef, efC = meshgen.ef_contacts(mesh, n)
+    ee, eeC = meshgen.ee_contacts(mesh, n)
+    vf, vfC = meshgen.vf_contacts(mesh, n)
+    P = mas_amd.SeSchwarzPreconditioner(max_levels=L)
+    P.m_positions, P.m_neighbours, P.m_edges, P.m_faces = mesh.pos, (mesh.starts, mesh.idx), mesh.edges, mesh.faces
+    P.AllocatePrecoditioner(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0])
+    P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, ef, ee, vf, efC, eeC, vfC)
+    o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], L, 4)
+    o.allocate(mesh)
+    o.prepare(mesh, ef=ef, ee=ee, vf=vf, efC=efC, eeC=eeC, vfC=vfC)
+    assert P.info()["num_stencils"] == o.num_stencils == 3 * n
+    compare_maps(P, o, mesh.nV)
+    for blk in range(P.info()["num_blocks"]):
+        A_g, A_o = P.block_matrix(blk), o.block_matrix(blk)
+        assert np.linalg.norm(A_g - A_o) <= 1e-6 * np.linalg.norm(A_o), blk
+    r = meshgen.residual(mesh.nV, 23)
+    assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
+
+
+def test_4m_tet_parity():
+    """BASELINE configs[4] on one GPU: the 160^3 Freudenthal lattice (valence
+    14), 4 levels (natural 5).  Level sizes are the survey probe's (patched
+    reference), maps bit-exact, z within 1e-5."""
+    from mas_amd import meshgen
+    mesh, cfg = meshgen.build_config("4M-tet")
+    P = _gpu(mesh, cfg["levels"])
+    inf = P.info()
+    ls = inf["level_size"]
+    assert mesh.nV == 4096000
+    assert [int(ls[l][0]) for l in range(1, 4)] == [208960, 10480, 574]
+    assert inf["num_blocks"] == 134876
+    o = _oracle(mesh, cfg["levels"], threads=16)
+    compare_maps(P, o, mesh.nV)
+    r = meshgen.residual(mesh.nV, 0x5EED + 4)
+    assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
