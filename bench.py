@@ -57,6 +57,21 @@ def algorithmic_bytes(info):
     return fine, apply
 
 
+def pmc_traffic_bytes(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (the
+    counters need their own rocprofv3 passes, so they cannot be read live)."""
+    path = os.path.join(REPO, "profiles", "round1", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        for name, v in d.items():
+            if kernel in name:
+                return int(v["corrected_bytes"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
 def cpu_baseline(mesh, cfg, contacts, r_np, steps):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from oracle import Oracle  # test infrastructure: the timed CPU baseline only
@@ -250,7 +265,10 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": None,
+            "traffic": pmc_traffic_bytes("k_solve_fine"),
+            "traffic_source": "profiles/round1/pmc_traffic.json: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                              "passes of this bench command, FETCH_SIZE x2 (gfx950 wide-read correction) + "
+                              "WRITE_SIZE, KB = 1024 B, per launch",
             "bytes_per_launch": fine_bytes,
             "avg_launch_ms": round(st["fine_ms_avg"], 5),
         },

@@ -14,13 +14,15 @@
 // single-thread order (vertex order, then ELL neighbour order; hash-map pushes
 // in node-id order, see oracle/mas_oracle.c), computed in parallel over
 // independent targets:
-//   k_level0      per vertex: block-0 diagonal and same-bank entries (single
-//                 writer), od(u) = diag + additional + level-0 entries
-//                 (oldDiagonal, .cpp:1270-1298), count of coarse edges
+//   k_level0_block  one workgroup per level-0 block, per vertex: block-0
+//                 diagonal and same-bank entries (single writer, tile in LDS,
+//                 block written whole), od(u) = diag + additional + level-0
+//                 entries (oldDiagonal, .cpp:1270-1298), count of coarse edges
 //   k_records     coarse edges (u, k) with first common-bank level 1..L-1, in
 //                 (u, k) order
-//   k_fold_entries  one thread per coarse entry (row, col), records sorted
-//                 stably by (row, col): entry += mat in (u, k) order
+//   k_fold_entries  one thread per coarse entry (row, col), (key, mat)
+//                 pairs sorted stably by key = (row, col): entry += mat in
+//                 (u, k) order
 //   k_diag1       one thread per level-0 bank: diag(anc1(u)) += od(u) (.cpp:1309-1312)
 //   k_term_*, k_table_fold  the diagTable fold (.cpp:1299-1343) per level-l
 //                 node (l >= 2): over member vertices in order, level-(l-1)
@@ -66,7 +68,15 @@ __device__ __forceinline__ void add_colmajor(float* e, const float* __restrict__
 // contacts (reference semantics, fp32 atomics)
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void k_collision_hessian(const DevStencil* __restrict__ st, int n,
+// Two passes over the stencils: ADDITIONAL (the per-vertex w^2 h terms and
+// the parent terms, read by the level-0 assembly and k_coarse_additional) runs
+// first; PAIRS (the h w_a w_b terms into the blocks) runs after the level-0
+// blocks are written whole, so the fine blocks need no memset and no
+// read-back.  For the fine entries this adds the contact terms after the CSR
+// terms instead of before (.cpp:1201-1271): a reassociation of fp32 sums the
+// reference's multi-threaded atomics do not fix either (B-10).
+enum { kContactAdditional = 1, kContactPairs = 2 };
+__global__ __launch_bounds__(256) void k_collision_hessian(const DevStencil* __restrict__ st, int n, int mode,
                                                            const int* __restrict__ gn, int L,
                                                            float* __restrict__ dense, float* __restrict__ additional) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -76,7 +86,7 @@ __global__ __launch_bounds__(256) void k_collision_hessian(const DevStencil* __r
     float hm[3][3];  // OuterProduct(d, d * stiff), SeMatrix.h:352-363
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) hm[r][c] = __fmul_rn(s.dir[r], ds[c]);
-    for (int it = 0; it < s.n; ++it) {  // .cpp:1214-1217: additional[idx] += h * w^2
+    for (int it = 0; mode == kContactAdditional && it < s.n; ++it) {  // .cpp:1214-1217: additional[idx] += h w^2
         const float w2 = __fmul_rn(s.w[it], s.w[it]);
         float* a = additional + 9 * (size_t)s.idx[it];
         for (int r = 0; r < 3; ++r)
@@ -88,15 +98,16 @@ __global__ __launch_bounds__(256) void k_collision_hessian(const DevStencil* __r
             unsigned my = (unsigned)s.idx[a], ot = (unsigned)s.idx[b];
             const int level = climb(gn, L, my, ot);
             if (level >= L) continue;
-            float* e0 = entry(dense, my, ot);
-            float* e1 = entry(dense, ot, my);
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) {
-                    const float t = __fmul_rn(ww, hm[r][c]);
-                    atomicAdd(e0 + r * 96 + c, t);
-                    atomicAdd(e1 + r * 96 + c, t);
-                }
-            if (level < L - 1) {
+            if (mode == kContactPairs) {
+                float* e0 = entry(dense, my, ot);
+                float* e1 = entry(dense, ot, my);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) {
+                        const float t = __fmul_rn(ww, hm[r][c]);
+                        atomicAdd(e0 + r * 96 + c, t);
+                        atomicAdd(e1 + r * 96 + c, t);
+                    }
+            } else if (level < L - 1) {
                 const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
                 for (int r = 0; r < 3; ++r)
                     for (int c = 0; c < 3; ++c) {
@@ -135,50 +146,86 @@ __global__ __launch_bounds__(256) void k_coarse_additional(int begin1, int tc, c
 // CSR Hessian (deterministic, reference order)
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void k_level0(int nV, int L, const int* __restrict__ s2o,
-                                                const int* __restrict__ nbrNum, const int* __restrict__ nbr,
-                                                const int* __restrict__ gn, const float* __restrict__ diag9,
-                                                const float* __restrict__ off9, const int* __restrict__ ranges,
-                                                const float* __restrict__ additional, float* __restrict__ dense,
-                                                float* __restrict__ od, int* __restrict__ recCnt) {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= nV) return;
-    const int o = s2o[v];
-    float acc[9];
-    const float* d = diag9 + 9 * (size_t)o;
-    const float* ad = additional + 9 * (size_t)v;
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);  // .cpp:1270
-    {
-        float* e = entry(dense, v, v);  // .cpp:1271
+// Level-0 assembly, one 64-lane workgroup per level-0 block; per vertex
+// (.cpp:1257-1297): diag + additional on its diagonal, every same-bank CSR
+// neighbour into its row, the running sum od(v) = diag + additional + those
+// neighbour blocks (the vertex's part of its level-1 diagonal, .cpp:1275-1282),
+// and the count of its coarse edge records.  The block's 96x96 tile is built
+// in LDS (vertex n adds only into its own rows 3n..3n+2, as in the
+// reference's owner loop) and written out whole
+// with coalesced stores, so the fine part of the dense buffer needs no memset
+// and no read-modify-write of scattered 3x3 entries (k_level0 moved 5 GB per
+// launch at 1M for 1.2 GB of blocks as a thread-per-vertex kernel).  The tile
+// starts from zeros; contact pair terms are added afterwards (see
+// k_collision_hessian).
+__global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* __restrict__ s2o,
+                                                     const int* __restrict__ nbrNum, const int* __restrict__ nbr,
+                                                     const float* __restrict__ diag9,
+                                                     const float* __restrict__ off9, const int* __restrict__ ranges,
+                                                     const float* __restrict__ additional,
+                                                     float* __restrict__ dense, float* __restrict__ od,
+                                                     int* __restrict__ recCnt) {
+    __shared__ __attribute__((aligned(16))) float tile[kDenseFloats];
+    const int lane = threadIdx.x;
+    const size_t blk = blockIdx.x;
+    float4* gblk = reinterpret_cast<float4*>(dense + blk * kDenseFloats);
+    float4* t4 = reinterpret_cast<float4*>(tile);
+    for (int q = lane; q < kDenseFloats / 4; q += 64) t4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    const int n = lane;
+    const int v = (int)blk * 32 + n;
+    if (n < 32 && v < nV) {
+        const int o = s2o[v];
+        float acc[9];
+        const float* d = diag9 + 9 * (size_t)o;
+        const float* ad = additional + 9 * (size_t)v;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);  // .cpp:1270
+        float* e = tile + (3 * n) * 96 + 3 * n;  // .cpp:1271
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], acc[r * 3 + c]);
-    }
-    const int num = nbrNum[v];
-    const size_t base = (size_t)ranges[o];
-    int cnt = 0;
-    for (int k = 1; k < num; ++k) {
-        unsigned my = (unsigned)v, ot = (unsigned)nbr[(size_t)k * nV + v];
-        const int level = climb(gn, L, my, ot);
-        if (level >= L) continue;
-        if (level == 0) {
-            const float* m = off9 + 9 * (base + k - 1);
-            add_colmajor(entry(dense, my, ot), m);
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[c * 3 + r]);
-        } else {
-            cnt++;
+        const int num = nbrNum[v];
+        const size_t base = (size_t)ranges[o];
+        int cnt = 0;
+        // neighbours in chunks of 4 with every load of the chunk issued first
+        // (the loop is latency-bound: one wave per block, 32 active lanes)
+        for (int k0 = 1; k0 < num; k0 += 4) {
+            unsigned ot[4];
+            float mm[4][9];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = k0 + j;
+                ot[j] = k < num ? (unsigned)nbr[(size_t)k * nV + v] : 0xffffffffu;
+                const float* m = off9 + 9 * (base + (k < num ? k - 1 : 0));
+#pragma unroll
+                for (int q = 0; q < 9; ++q) mm[j][q] = m[q];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (k0 + j >= num) break;
+                if ((ot[j] >> 5) == ((unsigned)v >> 5)) {  // same bank: level 0
+                    float* t = tile + (3 * n) * 96 + 3 * (ot[j] & 31);
+                    for (int r = 0; r < 3; ++r)
+                        for (int c = 0; c < 3; ++c) t[r * 96 + c] = __fadd_rn(t[r * 96 + c], mm[j][c * 3 + r]);
+                    for (int r = 0; r < 3; ++r)
+                        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], mm[j][c * 3 + r]);
+                } else {
+                    cnt++;  // a coarse edge record (k_records finds its level; level >= L: a dead record)
+                }
+            }
         }
+        for (int q = 0; q < 9; ++q) od[9 * (size_t)v + q] = acc[q];
+        recCnt[v] = cnt;
     }
-    for (int e = 0; e < 9; ++e) od[9 * (size_t)v + e] = acc[e];
-    recCnt[v] = cnt;
+    __syncthreads();
+    for (int q = lane; q < kDenseFloats / 4; q += 64) gblk[q] = t4[q];
 }
 
 __global__ __launch_bounds__(256) void k_records(int nV, int L, const int* __restrict__ s2o,
                                                  const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                  const int* __restrict__ gn, const int* __restrict__ ranges,
                                                  const int* __restrict__ recOff, EdgeRec* __restrict__ rec,
-                                                 unsigned long long* __restrict__ keys, int* __restrict__ ids) {
+                                                 unsigned long long* __restrict__ keys, int* __restrict__ mats) {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nV) return;
     const int o = s2o[v];
@@ -187,30 +234,34 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, const int* __res
     int w = recOff[v];
     for (int k = 1; k < num; ++k) {
         unsigned my = (unsigned)v, ot = (unsigned)nbr[(size_t)k * nV + v];
+        if ((my >> 5) == (ot >> 5)) continue;  // level 0: in the block (k_level0_block)
         const int level = climb(gn, L, my, ot);
-        if (level == 0 || level >= L) continue;
-        rec[w] = EdgeRec{level, (int)my, (int)ot, base + k - 1};
-        keys[w] = ((unsigned long long)my << 32) | ot;
-        ids[w] = w;
+        if (level >= L) {  // no common bank below L (.cpp:1286): a dead record, sorted last
+            rec[w] = EdgeRec{L, -1, -1, base + k - 1};
+            keys[w] = ~0ull;
+        } else {
+            rec[w] = EdgeRec{level, (int)my, (int)ot, base + k - 1};
+            keys[w] = ((unsigned long long)my << 32) | ot;
+        }
+        mats[w] = base + k - 1;  // sort payload: records of one entry stay in (u, k) order (stable sort)
         ++w;
     }
 }
 
 // one thread per run of equal (row, col) in the stably sorted record keys
 __global__ __launch_bounds__(256) void k_fold_entries(int n, const unsigned long long* __restrict__ keys,
-                                                      const int* __restrict__ ids, const EdgeRec* __restrict__ rec,
-                                                      const float* __restrict__ off9, float* __restrict__ dense) {
+                                                      const int* __restrict__ mats, const float* __restrict__ off9,
+                                                      float* __restrict__ dense) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const unsigned long long key = keys[i];
-    if (i > 0 && keys[i - 1] == key) return;
-    const EdgeRec r0 = rec[ids[i]];
-    float* e = entry(dense, (unsigned)r0.row, (unsigned)r0.col);
+    if (key == ~0ull || (i > 0 && keys[i - 1] == key)) return;
+    float* e = entry(dense, (unsigned)(key >> 32), (unsigned)(key & 0xffffffffu));
     float acc[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
     for (int j = i; j < n && keys[j] == key; ++j) {
-        const float* m = off9 + 9 * (size_t)rec[ids[j]].mat;
+        const float* m = off9 + 9 * (size_t)mats[j];
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[c * 3 + r]);
     }
@@ -341,7 +392,11 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         (rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
         (rc = ensure(h, h->recOff, (size_t)(nV + 1) * 4)) || (rc = ensure(h, h->tab, (size_t)(tc + 1) * 36)))
         return rc;
-    if ((rc = hip_check(h, hipMemsetAsync(h->dense.p, 0, denseBytes, s), "memset dense")) ||
+    // fine blocks are written whole by k_level0_block: zero only the coarse blocks
+    const size_t zeroFrom = (size_t)h->nFineBlk * kDenseFloats * 4;
+    if ((denseBytes > zeroFrom &&
+         (rc = hip_check(h, hipMemsetAsync(static_cast<char*>(h->dense.p) + zeroFrom, 0, denseBytes - zeroFrom, s),
+                         "memset dense"))) ||
         (rc = hip_check(h, hipMemsetAsync(h->additional.p, 0, (size_t)(tc + 1) * 36, s), "memset additional")) ||
         (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt")))
         return rc;
@@ -350,12 +405,15 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     const int* gn = P<int>(h->goingNext);
     const int begin1 = h->levelSize[3];
     if (h->nStencil) {
-        k_collision_hessian<<<cdiv(h->nStencil, 256), 256, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil, gn, L,
-                                                                   dense, add);
+        k_collision_hessian<<<cdiv(h->nStencil, 256), 256, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
+                                                                   kContactAdditional, gn, L, dense, add);
         if (tc > begin1) k_coarse_additional<<<cdiv(tc - begin1, 256), 256, 0, s>>>(begin1, tc, gn, add, dense);
     }
-    k_level0<<<cdiv(nV, 256), 256, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), gn, d_diag9,
-                                           d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt));
+    k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
+                                              d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt));
+    if (h->nStencil)
+        k_collision_hessian<<<cdiv(h->nStencil, 256), 256, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
+                                                                   kContactPairs, gn, L, dense, add);
     if (L == 1) return hip_check(h, hipGetLastError(), "assembly kernels");
 
     // coarse edge records in (u, k) order
@@ -393,7 +451,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                             "record sort")))
             return rc;
         k_fold_entries<<<cdiv(nRec, 256), 256, 0, s>>>(nRec, P<unsigned long long>(h->recKeysSorted),
-                                                       P<int>(h->recIdsSorted), rec, d_off9, dense);
+                                                       P<int>(h->recIdsSorted), d_off9, dense);
     }
     k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
 

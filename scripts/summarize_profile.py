@@ -32,7 +32,7 @@ lines += ["", "## HBM traffic per launch (separate --pmc passes; FETCH_SIZE x 2 
 out = {}
 for name in sorted({k[0] for k in pmc}):
     f = pmc.get((name, "FETCH_SIZE"), [0]); w = pmc.get((name, "WRITE_SIZE"), [0])
-    if len(f) < 5:
+    if len(f) < 3:
         continue
     fm, wm = sum(f) / len(f), sum(w) / len(w)
     tb = (2 * fm + wm) * 1024
