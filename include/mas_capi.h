@@ -178,6 +178,18 @@ int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r
 int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gathered4, const float* d_r4,
                            float* d_z4, void* stream);
 
+/* ---- fixture / wire format ----
+ * A prepared handle as one versioned, checksummed blob (header "MASBLOB",
+ * version 1, FNV-1a 64 over the payload): level sizes, Morton codes, both
+ * permutations, CoarseSpaceTables, goingNext, coarseTables, fine connect
+ * masks, the apply maps and the packed inverses (630 MB at 1M).  Loading it
+ * into any handle makes that handle prepared without Allocate/Prepare inputs
+ * (warm start, cross-box golden comparison); mas_apply*, mas_shard_*,
+ * mas_get_maps and mas_get_block_inverse work on it, a new Prepare needs
+ * mas_allocate first.  Host buffers. */
+int mas_blob_size(mas_handle h, size_t* out_bytes);
+int mas_save_blob(mas_handle h, void* dst, size_t capacity, size_t* written);
+int mas_load_blob(mas_handle h, const void* src, size_t size);
 /* introspection / parity */
 int mas_get_info(mas_handle h, mas_info* out);
 int mas_get_stats(mas_handle h, mas_stats* out);

@@ -146,6 +146,12 @@ int mas_allocate(mas_handle h, int nV, int nE, int nF, const float* pos4, const 
     if (h->allocated && nV != h->nV)
         return fail(h, MAS_ERR_STATE, "mas_allocate: numVerts must stay fixed after the first call");
     hipSetDevice(h->device);
+    if (h->fromBlob) {  // a restored handle starts over as a fresh one
+        h->fromBlob = false;
+        h->allocated = false;
+        h->prepared = false;
+        h->allocCalls = 0;
+    }
     h->nE = nE;
     h->nF = nF;
     h->nV = nV;
@@ -155,7 +161,7 @@ int mas_allocate(mas_handle h, int nV, int nE, int nF, const float* pos4, const 
 static int prepare_common(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges, const void* ef,
                           const void* ee, const void* vf, const unsigned* efC, const unsigned* eeC,
                           const unsigned* vfC, hipStream_t s) {
-    if (!h->allocated) return fail(h, MAS_ERR_STATE, "prepare before allocate");
+    if (!h->allocated || h->fromBlob) return fail(h, MAS_ERR_STATE, "prepare before allocate");
     return run_prepare(h, d_diag9, d_off9, d_ranges, ef, ee, vf, efC, eeC, vfC, s);
 }
 
@@ -163,7 +169,7 @@ int mas_prepare(mas_handle h, const float* diag9, const float* off9, const int* 
                 const void* vf, const unsigned* efC, const unsigned* eeC, const unsigned* vfC) {
     if (!h) return MAS_ERR_ARG;
     if (!diag9 || !off9 || !ranges) return fail(h, MAS_ERR_ARG, "mas_prepare: null Hessian pointer");
-    if (!h->allocated) return fail(h, MAS_ERR_STATE, "prepare before allocate");
+    if (!h->allocated || h->fromBlob) return fail(h, MAS_ERR_STATE, "prepare before allocate");
     hipSetDevice(h->device);
     const size_t nV = h->nV, nnz = h->nnz;
     MAS_TRY(ensure(h, h->diagStage, nV * 36));
@@ -208,7 +214,7 @@ int mas_pcg_solve_device(mas_handle h, const float* d_diag9, const float* d_off9
         return fail(h, MAS_ERR_ARG, "mas_pcg_solve_device: vectors must be 16-byte aligned");
     if (max_iters < 0 || !(tol >= 0.0f)) return fail(h, MAS_ERR_ARG, "mas_pcg_solve_device: bad max_iters / tol");
     if (precondition && !h->prepared) return fail(h, MAS_ERR_STATE, "preconditioned solve before prepare");
-    if (!h->allocated) return fail(h, MAS_ERR_STATE, "solve before allocate");
+    if (!h->allocated || h->fromBlob) return fail(h, MAS_ERR_STATE, "solve before allocate (needs the neighbour ids)");
     hipSetDevice(h->device);
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     return run_pcg(h, d_diag9, d_off9, d_ranges, reinterpret_cast<float4*>(d_x4),
@@ -219,7 +225,7 @@ int mas_pcg_solve(mas_handle h, const float* diag9, const float* off9, const int
                   int max_iters, float tol, int precondition, mas_pcg_result* out) {
     if (!h) return MAS_ERR_ARG;
     if (!diag9 || !off9 || !ranges || !x4 || !b4) return fail(h, MAS_ERR_ARG, "mas_pcg_solve: null pointer");
-    if (!h->allocated) return fail(h, MAS_ERR_STATE, "solve before allocate");
+    if (!h->allocated || h->fromBlob) return fail(h, MAS_ERR_STATE, "solve before allocate (needs the neighbour ids)");
     hipSetDevice(h->device);
     const size_t nV = h->nV, nnz = h->nnz, vb = nV * 16;
     MAS_TRY(ensure(h, h->diagStage, nV * 36));
@@ -342,7 +348,7 @@ int mas_get_maps(mas_handle h, uint64_t* morton, int* s2o, int* o2s, int* cst, i
 
 int mas_get_neighbors(mas_handle h, int* nbr_num, int* nbr) {
     if (!h) return MAS_ERR_ARG;
-    if (!h->allocated) return fail(h, MAS_ERR_STATE, "neighbors before allocate");
+    if (!h->allocated || !h->nbr.p || h->fromBlob) return fail(h, MAS_ERR_STATE, "neighbors before allocate");
     hipSetDevice(h->device);
     hipStreamSynchronize(h->stream);
     if (nbr_num) MAS_TRY(hip_check(h, hipMemcpy(nbr_num, h->nbrNum.p, (size_t)h->nV * 4, hipMemcpyDeviceToHost), "D2H"));
@@ -353,7 +359,8 @@ int mas_get_neighbors(mas_handle h, int* nbr_num, int* nbr) {
 
 int mas_get_block_matrix(mas_handle h, int blk, float* out96) {
     if (!h || !out96) return MAS_ERR_ARG;
-    if (!h->prepared) return fail(h, MAS_ERR_STATE, "block matrix before prepare");
+    if (!h->prepared || h->fromBlob || !h->dense.p)
+        return fail(h, MAS_ERR_STATE, "block matrix before prepare (a restored blob holds no assembly blocks)");
     if (blk < 0 || blk >= h->nBlk) return fail(h, MAS_ERR_ARG, "block index out of range");
     hipSetDevice(h->device);
     hipStreamSynchronize(h->stream);

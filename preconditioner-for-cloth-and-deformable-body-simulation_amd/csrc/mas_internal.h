@@ -57,6 +57,7 @@ struct mas_context {
     int natL = 0, L = 0, maxNbr = 0;
     int allocCalls = 0;   // reference m_frameIndex semantics (B-1)
     bool allocated = false, prepared = false, profiling = false;
+    bool fromBlob = false;  // restored by mas_load_blob: applies, no Prepare inputs (blob.hip)
     int overlap = 0;      // 1: coarse chain on stream2 beside the fine blocks (measured slower: 150.8 vs 124.3 us at 1M; env MAS_OVERLAP)
     hipStream_t stream2 = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;

@@ -33,7 +33,7 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
            "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_get_info",
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
            "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
-           "mas_pcg_solve_device", "mas_pcg_solve"]
+           "mas_pcg_solve_device", "mas_pcg_solve", "mas_blob_size", "mas_save_blob", "mas_load_blob"]
 
 
 class mas_config(ctypes.Structure):
@@ -118,6 +118,9 @@ def lib():
         F = ctypes.c_float
         L.mas_pcg_solve_device.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result), P]
         L.mas_pcg_solve.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result)]
+        L.mas_blob_size.argtypes = [P, ctypes.POINTER(ctypes.c_size_t)]
+        L.mas_save_blob.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+        L.mas_load_blob.argtypes = [P, P, ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -241,6 +244,21 @@ class SeSchwarzPreconditioner:
                                                  _ptr(b), int(max_iters), float(tol), int(bool(precondition)),
                                                  ctypes.byref(res), _ptr(stream)), "pcg_solve_device")
         return res.as_dict()
+
+    # ---- fixture / wire format ----
+    def save_blob(self) -> np.ndarray:
+        """The prepared handle as a versioned blob (uint8 array)."""
+        n = ctypes.c_size_t()
+        self._check(self._L.mas_blob_size(self.h, ctypes.byref(n)), "blob_size")
+        buf = np.empty(n.value, dtype=np.uint8)
+        w = ctypes.c_size_t()
+        self._check(self._L.mas_save_blob(self.h, _ptr(buf), n.value, ctypes.byref(w)), "save_blob")
+        return buf[: w.value]
+
+    def load_blob(self, blob):
+        b = np.ascontiguousarray(np.frombuffer(blob, dtype=np.uint8) if isinstance(blob, (bytes, bytearray))
+                                 else blob, dtype=np.uint8)
+        self._check(self._L.mas_load_blob(self.h, _ptr(b), b.nbytes), "load_blob")
 
     # ---- introspection ----
     def set_profiling(self, on: bool):
