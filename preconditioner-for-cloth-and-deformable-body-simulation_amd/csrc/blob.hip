@@ -180,6 +180,8 @@ int blob_load(mas_context* h, const void* src, size_t size) {
         (rc = ensure(h, h->Zc, (size_t)(nCoarse > 0 ? nCoarse : 1) * 16)))
         return rc;
     if (nCoarse > 0 && (rc = hip_check(h, hipMemset(h->Rc.p, 0, (size_t)nCoarse * 16), "memset Rc"))) return rc;
+    if ((rc = build_l1src(h, h->stream)) || (rc = hip_check(h, hipStreamSynchronize(h->stream), "blob sync")))
+        return rc;
     h->shardWorld = 0;
     h->fromBlob = true;
     h->allocated = true;  // maps are valid

@@ -1,15 +1,15 @@
 // k_apply.hip -- Preconditioning (.cpp:100-110, 1548-1719): the hot path.
 //
 // Per apply, L launches on one stream:
-//   k_coarse<level 1>   per level-1 block (one wave): R1 of its 32 nodes from
+//   k_coarse_l1         per level-1 block (one wave): R1 of its 32 nodes from
 //                       r gathered through the Morton map, summed per parent
 //                       in lane order from +0 exactly as the reference's owner
 //                       loop (BuildResidualHierarchy .cpp:1558-1574); then
 //                       Z1 = Inv_b R1 (SchwarzLocalXSym .cpp:1600-1696).
-//   k_coarse<level l>   l = 2..L-1: R_l from R_{l-1} the same way (level 2 is
-//                       the reference's level-1-id-order sum, .cpp:1581-1590;
-//                       level >= 3 sums R_{l-1}, same value up to fp
-//                       association), then Z_l.
+//   k_coarse_up         l = 2..L-1, one launch per level: R_l from
+//                       R_{l-1} the same way (level 2 is the reference's
+//                       level-1-id-order sum, .cpp:1581-1590; level >= 3 sums
+//                       R_{l-1}, same value up to fp association), then Z_l.
 //   k_solve_fine        every level-0 block fused with the gather r[s2o[v]]
 //                       and the prolongation z[s2o[v]] = Z0 + Z1[a1] + Z2[a2]
 //                       + Z3[a3] (CollectFinalZ .cpp:1698-1719, min(L,4)-1
@@ -77,52 +77,92 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __re
     solve_fine_body<NPROL, VAR>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z);
 }
 
-// One coarse level l >= 1, one wave per 32-node block; lane n (half 0) owns
-// node P = 32 blk + n.  members[P] = (child bank, component mask): the
-// children of P are exactly the lanes of that mask (they are the connected
-// component the clustering merged into P, .cpp:590-625 / 917-954).  Every
-// child value is gathered up front (one latency), then lane n adds its
-// children in lane order from +0 -- the reference's accumulation order for
-// level 1 (.cpp:1560-1572) and level 2 (level-1 id order, .cpp:1581-1590);
-// level >= 3 sums R_{l-1} (the reference sums R_1 directly: same value up
-// to fp association).  Then Z_l = Inv_b R_l; R_l and Z_l are stored.
-template <bool FROM_VERTS>
-__global__ __launch_bounds__(kApplyThreads) void k_coarse(const float4* __restrict__ inv, int blkBegin, int nb,
-                                                         int count, const int2* __restrict__ members,
-                                                         int childBegin, const int* __restrict__ s2o,
-                                                         const float4* __restrict__ r, float4* __restrict__ rc,
-                                                         float4* __restrict__ zc, int begin1) {
-    const int lane = threadIdx.x & 63, n = lane & 31;
-    const int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
-    if (w >= nb) return;  // wave-uniform
-    const int blk = blkBegin + w;
+// Coarse levels, one wave per 32-node block; lane n (half 0) owns node
+// P = 32 blk + n.  The children of P are exactly the lanes of one component
+// of one child bank (the connected component the clustering merged into P,
+// .cpp:590-625 / 917-954).  Every child value is gathered up front (one
+// latency), then lane n adds its children in lane order from +0 -- the
+// reference's accumulation order for level 1 (.cpp:1560-1572) and level 2
+// (level-1 id order, .cpp:1581-1590); level >= 3 sums R_{l-1} (the reference
+// sums R_1 directly: same value up to fp association).  Then
+// Z_l = Inv_b R_l; R_l and Z_l are stored.
+//
+// Level 1 reads its children's original vertex ids from l1src (32 ids per
+// level-1 node, -1 where the lane is not a child; built at Prepare), so the
+// r gather is the second dependent load of the wave instead of the third
+// (members -> s2o -> r).  Levels >= 2 read members = (child bank, mask).
+__device__ __forceinline__ void coarse_finish(const float (&g)[kRecord], const float (&tl)[3], int lane, int n,
+                                              int node, bool own, float ax, float ay, float az,
+                                              float4* __restrict__ rc, float4* __restrict__ zc, int begin1) {
+    // half 1 takes node n's residual from lane n
+    ax = __shfl(ax, n);
+    ay = __shfl(ay, n);
+    az = __shfl(az, n);
+    const float3 out = block_solve(g, tl, make_float3(ax, ay, az), lane);
+    if (lane < 32) {
+        rc[node - begin1] = make_float4(ax, ay, az, 0.f);
+        zc[node - begin1] = make_float4(out.x, out.y, out.z, 0.f);
+    }
+    (void)own;
+}
+
+__device__ __forceinline__ void coarse_block_l1(const float4* __restrict__ inv, int blk, int blkBegin, int count,
+                                                const int* __restrict__ l1src, const float4* __restrict__ r,
+                                                float4* __restrict__ rc, float4* __restrict__ zc, int begin1,
+                                                int lane) {
+    const int n = lane & 31;
+    const int node = blk * 32 + n;
+    float g[kRecord], tl[3];
+    load_record<true>(inv, blk, lane, g, tl);
+    const bool own = lane < 32 && (node - blkBegin * 32) < count;
+    int src[32];
+    const int4* s4 = reinterpret_cast<const int4*>(l1src + (size_t)(node - blkBegin * 32) * 32);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int4 t = own ? s4[q] : make_int4(-1, -1, -1, -1);
+        src[4 * q + 0] = t.x;
+        src[4 * q + 1] = t.y;
+        src[4 * q + 2] = t.z;
+        src[4 * q + 3] = t.w;
+    }
+    float vx[32], vy[32], vz[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (src[j] >= 0) v = r[src[j]];
+        vx[j] = v.x;
+        vy[j] = v.y;
+        vz[j] = v.z;
+    }
+    float ax = 0.f, ay = 0.f, az = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        if (src[j] >= 0) {
+            ax = __fadd_rn(ax, vx[j]);
+            ay = __fadd_rn(ay, vy[j]);
+            az = __fadd_rn(az, vz[j]);
+        }
+    }
+    coarse_finish(g, tl, lane, n, node, own, ax, ay, az, rc, zc, begin1);
+}
+
+__device__ __forceinline__ void coarse_block_up(const float4* __restrict__ inv, int blk, int blkBegin, int count,
+                                                const int2* __restrict__ members, int childBegin,
+                                                float4* __restrict__ rc, float4* __restrict__ zc, int begin1,
+                                                int lane) {
+    const int n = lane & 31;
     const int node = blk * 32 + n;
     float g[kRecord], tl[3];
     load_record<true>(inv, blk, lane, g, tl);
     const bool own = lane < 32 && (node - blkBegin * 32) < count;
     const int2 mb = own ? members[node - begin1] : make_int2(0, 0);
     const unsigned msk = (unsigned)mb.y;
-    const int base = mb.x * 32;
-    int src[32];
-    if (FROM_VERTS) {  // the bank's 32 Morton->original ids: 8 x 16-byte loads
-        const int4* s4 = reinterpret_cast<const int4*>(s2o + base);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int4 t = s4[q];
-            src[4 * q + 0] = t.x;
-            src[4 * q + 1] = t.y;
-            src[4 * q + 2] = t.z;
-            src[4 * q + 3] = t.w;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) src[j] = childBegin + base + j - begin1;
-    }
+    const int base = childBegin + mb.x * 32 - begin1;
     float vx[32], vy[32], vz[32];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if ((msk >> j) & 1u) v = FROM_VERTS ? r[src[j]] : rc[src[j]];
+        if ((msk >> j) & 1u) v = rc[base + j];
         vx[j] = v.x;
         vy[j] = v.y;
         vz[j] = v.z;
@@ -136,15 +176,25 @@ __global__ __launch_bounds__(kApplyThreads) void k_coarse(const float4* __restri
             az = __fadd_rn(az, vz[j]);
         }
     }
-    // half 1 takes node n's residual from lane n
-    ax = __shfl(ax, n);
-    ay = __shfl(ay, n);
-    az = __shfl(az, n);
-    const float3 out = block_solve(g, tl, make_float3(ax, ay, az), lane);
-    if (lane < 32) {
-        rc[node - begin1] = make_float4(ax, ay, az, 0.f);
-        zc[node - begin1] = make_float4(out.x, out.y, out.z, 0.f);
-    }
+    coarse_finish(g, tl, lane, n, node, own, ax, ay, az, rc, zc, begin1);
+}
+
+__global__ __launch_bounds__(kApplyThreads) void k_coarse_l1(const float4* __restrict__ inv, int blkBegin, int nb,
+                                                            int count, const int* __restrict__ l1src,
+                                                            const float4* __restrict__ r, float4* __restrict__ rc,
+                                                            float4* __restrict__ zc, int begin1) {
+    const int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
+    if (w >= nb) return;  // wave-uniform
+    coarse_block_l1(inv, blkBegin + w, blkBegin, count, l1src, r, rc, zc, begin1, threadIdx.x & 63);
+}
+
+__global__ __launch_bounds__(kApplyThreads) void k_coarse_up(const float4* __restrict__ inv, int blkBegin, int nb,
+                                                            int count, const int2* __restrict__ members,
+                                                            int childBegin, float4* __restrict__ rc,
+                                                            float4* __restrict__ zc, int begin1) {
+    const int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
+    if (w >= nb) return;  // wave-uniform
+    coarse_block_up(inv, blkBegin + w, blkBegin, count, members, childBegin, rc, zc, begin1, threadIdx.x & 63);
 }
 
 // Prepare-time: members[P] = (bank, closure mask) of the component that
@@ -184,7 +234,10 @@ void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* 
     }
 }
 
-// coarse levels lFirst..L-1 with k_coarse (level 1 from the vertices)
+// coarse levels lFirst..L-1: level 1 from the vertices (k_coarse_l1), then
+// one k_coarse_up launch per level.  (Levels >= 2 in one workgroup separated
+// by barriers measured 99 us at 1M: a 1024-thread workgroup caps the block
+// solve at 128 VGPRs and it spills; fewer waves serialise the blocks.)
 void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s) {
     const float4* inv = P<float4>(h->inv);
     float4* rc = P<float4>(h->Rc);
@@ -194,12 +247,11 @@ void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStre
         const int cnt = h->levelSize[2 * l], beg = h->levelSize[2 * l + 1];
         const int nb = ceil32(cnt) / 32;
         if (l == 1)
-            k_coarse<true><<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int2>(h->members), 0,
-                                                                          P<int>(h->s2o), d_r, rc, zc, begin1);
+            k_coarse_l1<<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int>(h->l1src), d_r,
+                                                                      rc, zc, begin1);
         else
-            k_coarse<false><<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int2>(h->members),
-                                                                           h->levelSize[2 * (l - 1) + 1], nullptr,
-                                                                           nullptr, rc, zc, begin1);
+            k_coarse_up<<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int2>(h->members),
+                                                                      h->levelSize[2 * (l - 1) + 1], rc, zc, begin1);
     }
 }
 
@@ -275,7 +327,33 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     return hip_check(h, hipGetLastError(), "apply kernels");
 }
 
-// Apply-side tables, built once per Prepare: members[] for every coarse node.
+// l1src[P][j] = original id of lane j of P's bank if that lane is a child of
+// level-1 node P, else -1 (P = level-1 local id; padding nodes all -1).
+__global__ __launch_bounds__(256) void k_l1src(int n1Pad, int n1, const int2* __restrict__ members,
+                                               const int* __restrict__ s2o, int* __restrict__ l1src) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n1Pad * 32) return;
+    const int P = t >> 5, j = t & 31;
+    int id = -1;
+    if (P < n1) {
+        const int2 mb = members[P];
+        if (((unsigned)mb.y >> j) & 1u) id = s2o[mb.x * 32 + j];
+    }
+    l1src[t] = id;
+}
+
+int build_l1src(mas_context* h, hipStream_t s) {
+    if (h->L < 2) return MAS_OK;
+    const int n1 = h->levelSize[2], n1Pad = ceil32(n1);
+    int rc = ensure(h, h->l1src, (size_t)n1Pad * 32 * 4);
+    if (rc) return rc;
+    k_l1src<<<cdiv((long long)n1Pad * 32, 256), 256, 0, s>>>(n1Pad, n1, P<int2>(h->members), P<int>(h->s2o),
+                                                             P<int>(h->l1src));
+    return hip_check(h, hipGetLastError(), "l1src");
+}
+
+// Apply-side tables, built once per Prepare: members[] for every coarse node,
+// l1src for level 1.
 int prepare_apply_tables(mas_context* h, hipStream_t s) {
     const int nV = h->nV, L = h->L;
     const int begin1 = h->levelSize[3];
@@ -291,7 +369,8 @@ int prepare_apply_tables(mas_context* h, hipStream_t s) {
         const unsigned* masks = l == 1 ? P<unsigned>(h->fineMask) : P<unsigned>(h->coarseMask) + (childBegin - begin1);
         k_members<<<cdiv(nChild, 256), 256, 0, s>>>(nChild, childBegin, masks, gn, begin1, P<int2>(h->members));
     }
-    return hip_check(h, hipGetLastError(), "apply tables");
+    if ((rc = hip_check(h, hipGetLastError(), "apply tables"))) return rc;
+    return build_l1src(h, s);
 }
 
 }  // namespace mas

@@ -4,11 +4,11 @@
 // components of one level-0 bank and their ids are assigned in bank order, so
 // the rank's level-1 nodes are the contiguous segment [l1_first[fb0],
 // l1_first[fb1]).  Per apply and rank:
-//   k_restrict_seg   R1 of the own segment (same ordered sums as k_coarse<1>)
+//   k_restrict_seg   R1 of the own segment (same ordered sums as k_coarse_l1)
 //   -- caller: allgather of the padded segments over RCCL --
 //   k_unpack_r1      gathered segments -> R1 of every level-1 node
 //   k_solve_nodes    own level-1 blocks: Z1 = Inv R1
-//   k_coarse<false>  every block of levels >= 2 (tiny, redundant on all ranks)
+//   k_coarse_up      every block of levels >= 2 (tiny, redundant on all ranks)
 //   k_solve_fine     own level-0 blocks + prolongation, z of own vertices
 // Every value is computed by the same kernel arithmetic as the unsharded
 // apply, so the union of the ranks' outputs is bitwise equal to it.

@@ -78,7 +78,7 @@ struct mas_context {
     mas::Buffer dense, inv, slotTable;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
-    mas::Buffer Rc, Zc, members, coarseMask, shardOff;
+    mas::Buffer Rc, Zc, members, coarseMask, shardOff, l1src;
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     std::vector<int> l1First;  // first level-1 local id per level-0 bank (+ n1), for sharding
     int shardWorld = 0;
@@ -100,7 +100,7 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &l1src, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -133,6 +133,7 @@ int run_factor(mas_context* h, hipStream_t s);
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s);
 int upload_slot_table(mas_context* h);
 int prepare_apply_tables(mas_context* h, hipStream_t s);
+int build_l1src(mas_context* h, hipStream_t s);
 int compute_l1_first(mas_context* h, hipStream_t s);
 int copy_block_inverse(mas_context* h, int blk, float* out96);
 int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,
