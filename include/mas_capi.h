@@ -111,8 +111,9 @@ int mas_prepare(mas_handle h, const float* diag9, const float* off9, const int* 
                 const void* ee, const void* vf, const unsigned* ef_counts, const unsigned* ee_counts,
                 const unsigned* vf_counts);
 
-/* PreparePreconditioner with device pointers.  Contact records stay host
- * pointers (they are small and their totals drive the launch sizes). */
+/* PreparePreconditioner with device pointers.  The contact records and their
+ * count arrays may be host or device pointers (e.g. the output buffers of a
+ * GPU collision-detection pass); only the totals are read back. */
 int mas_prepare_device(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges,
                        const void* ef, const void* ee, const void* vf, const unsigned* ef_counts,
                        const unsigned* ee_counts, const unsigned* vf_counts, void* stream);

@@ -247,9 +247,27 @@ static int read_int(mas_context* h, const int* dptr, int* out, hipStream_t s) {
     return hip_check(h, hipStreamSynchronize(s), "level sync");
 }
 
+// Contact records and their count arrays may live on the host or on the
+// device (e.g. straight from a GPU collision-detection pass):
+// totals are read with one 4-byte copy of unified addressing, records are
+// staged with hipMemcpyDefault.
+static long long count_total(mas_context* h, const unsigned* c, int at) {
+    if (!c) return 0;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, c) == hipSuccess && a.type == hipMemoryTypeDevice) {
+        unsigned v = 0;
+        if (hipMemcpy(&v, c + at, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        return v;
+    }
+    (void)hipGetLastError();  // a host pointer may leave "invalid value" behind
+    return c[at];
+}
+
 int build_stencils(mas_context* h, const void* ef, const void* ee, const void* vf, const unsigned* efC,
                    const unsigned* eeC, const unsigned* vfC, hipStream_t s) {
-    long long efNum = efC ? efC[h->nE] : 0, eeNum = eeC ? eeC[h->nE] : 0, vfNum = vfC ? vfC[h->nV] : 0;
+    long long efNum = count_total(h, efC, h->nE), eeNum = count_total(h, eeC, h->nE),
+              vfNum = count_total(h, vfC, h->nV);
+    if (efNum < 0 || eeNum < 0 || vfNum < 0) return fail(h, MAS_ERR_HIP, "reading contact counts");
     long long total = efNum + eeNum + vfNum;
     const long long maxStencil = (long long)h->nV * 32;  // .cpp:187-188
     h->nStencil = 0;
@@ -271,11 +289,11 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
         (rc = ensure(h, h->stencils, (size_t)total * sizeof(DevStencil))))
         return rc;
     unsigned char* raw = P<unsigned char>(h->rawContacts);
-    if (efNum && (rc = hip_check(h, hipMemcpyAsync(raw, ef, efNum * 48, hipMemcpyHostToDevice, s), "H2D ef"))) return rc;
-    if (eeNum && (rc = hip_check(h, hipMemcpyAsync(raw + efNum * 48, ee, eeNum * 48, hipMemcpyHostToDevice, s), "H2D ee")))
+    if (efNum && (rc = hip_check(h, hipMemcpyAsync(raw, ef, efNum * 48, hipMemcpyDefault, s), "stage ef"))) return rc;
+    if (eeNum && (rc = hip_check(h, hipMemcpyAsync(raw + efNum * 48, ee, eeNum * 48, hipMemcpyDefault, s), "stage ee")))
         return rc;
-    if (vfNum && (rc = hip_check(h, hipMemcpyAsync(raw + (efNum + eeNum) * 48, vf, vfNum * 48, hipMemcpyHostToDevice, s),
-                                 "H2D vf")))
+    if (vfNum && (rc = hip_check(h, hipMemcpyAsync(raw + (efNum + eeNum) * 48, vf, vfNum * 48, hipMemcpyDefault, s),
+                                 "stage vf")))
         return rc;
     const int n = (int)total;
     k_stencil_flags<<<cdiv(n, 256), 256, 0, s>>>(raw, (int)efNum, (int)eeNum, n, h->nV, h->nE, h->nF,

@@ -193,7 +193,10 @@ class SeSchwarzPreconditioner:
 
     def PreparePreconditionerDevice(self, d_diag, d_off, d_ranges, efSets=None, eeSets=None, vfSets=None,
                                     efCounts=None, eeCounts=None, vfCounts=None, stream=None):
-        efC, eeC, vfC = (_c(x, np.uint32) for x in (efCounts, eeCounts, vfCounts))
+        """Device Hessian; contact records / counts may be host arrays or device
+        tensors (e.g. a GPU collision pass's output buffers)."""
+        efC, eeC, vfC = (x if (x is None or hasattr(x, "data_ptr") or isinstance(x, int)) else _c(x, np.uint32)
+                         for x in (efCounts, eeCounts, vfCounts))
         self._check(self._L.mas_prepare_device(self.h, _ptr(d_diag), _ptr(d_off), _ptr(d_ranges), _ptr(efSets),
                                                _ptr(eeSets), _ptr(vfSets), _ptr(efC), _ptr(eeC), _ptr(vfC),
                                                _ptr(stream)), "PreparePreconditionerDevice")

@@ -195,3 +195,29 @@ def test_4m_tet_parity():
     compare_maps(P, o, mesh.nV)
     r = meshgen.residual(mesh.nV, 0x5EED + 4)
     assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
+
+
+def test_device_resident_contact_records():
+    """contact records and counts handed over in device memory
+    (as a GPU collision pass would) give the same preconditioner as host
+    records: same stencils, z equal up to the fp32 contact atomics' order."""
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(64)
+    ef, efC = meshgen.ef_contacts(mesh, 150)
+    vf, vfC = meshgen.vf_contacts(mesh, 150)
+    P = _gpu(mesh, 0)
+    P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, ef, None, vf, efC, None, vfC)
+    Q = _gpu(mesh, 0)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).cuda()
+    d_ef, d_efC, d_vf, d_vfC = dev(ef), dev(efC), dev(vf), dev(vfC)
+    dd = torch.from_numpy(np.ascontiguousarray(mesh.diag, np.float32)).cuda()
+    do = torch.from_numpy(np.ascontiguousarray(mesh.off, np.float32)).cuda()
+    dr = torch.from_numpy(np.ascontiguousarray(mesh.starts, np.int32)).cuda()
+    torch.cuda.synchronize()
+    Q.PreparePreconditionerDevice(dd, do, dr, d_ef, None, d_vf, d_efC, None, d_vfC)
+    torch.cuda.synchronize()
+    assert Q.info()["num_stencils"] == P.info()["num_stencils"] == 300
+    r = meshgen.residual(mesh.nV, 41)
+    assert rel_err(Q.Preconditioning(None, r), P.Preconditioning(None, r)) <= 1e-6
