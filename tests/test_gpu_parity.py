@@ -221,3 +221,61 @@ def test_device_resident_contact_records():
     assert Q.info()["num_stencils"] == P.info()["num_stencils"] == 300
     r = meshgen.residual(mesh.nV, 41)
     assert rel_err(Q.Preconditioning(None, r), P.Preconditioning(None, r)) <= 1e-6
+
+
+def test_periodic_resort():
+    """with resort_period = 0 (reference behaviour) a
+    later Allocate keeps the first Morton order; with resort_period = k the
+    k-th later call re-sorts, and the handle then matches a fresh one (and the
+    oracle) built on the moved positions."""
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(40)
+    moved = mesh.pos.copy()
+    moved[:, 0] = 1.0 - moved[:, 0]          # mirror x: a different Morton order
+    moved[:, 2] = 0.002 * np.sin(7.0 * moved[:, 1])
+
+    def handle(period):
+        P = mas_amd.SeSchwarzPreconditioner(resort_period=period)
+        P.m_positions, P.m_neighbours = mesh.pos, (mesh.starts, mesh.idx)
+        P.m_edges, P.m_faces = mesh.edges, mesh.faces
+        P.AllocatePrecoditioner(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0])
+        P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
+        return P
+
+    def realloc(P):
+        P.AllocatePrecoditioner(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0])
+        P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
+
+    first = handle(0).maps()["s2o"]
+    fresh = mas_amd.SeSchwarzPreconditioner()
+    fresh.m_positions, fresh.m_neighbours = moved, (mesh.starts, mesh.idx)
+    fresh.m_edges, fresh.m_faces = mesh.edges, mesh.faces
+    fresh.AllocatePrecoditioner(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0])
+    fresh.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
+    assert not np.array_equal(fresh.maps()["s2o"], first)
+
+    P0 = handle(0)
+    P0.m_positions = moved
+    realloc(P0)
+    np.testing.assert_array_equal(P0.maps()["s2o"], first)          # B-1 reproduced
+
+    P2 = handle(2)
+    P2.m_positions = moved
+    realloc(P2)                                                     # call 2: no sort
+    np.testing.assert_array_equal(P2.maps()["s2o"], first)
+    realloc(P2)                                                     # call 3: re-sort
+    g, f = P2.maps(), fresh.maps()
+    for k in ("morton", "s2o", "o2s", "coarse_space_tables", "going_next", "fine_connect_mask"):
+        np.testing.assert_array_equal(g[k], f[k], err_msg=k)
+    r = meshgen.residual(mesh.nV, 5)
+    np.testing.assert_array_equal(P2.Preconditioning(None, r), fresh.Preconditioning(None, r))
+    # and the oracle built on the moved positions agrees
+    from oracle import Oracle
+    import dataclasses
+    mesh_moved = dataclasses.replace(mesh, pos=moved)
+    o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], 0, 2)
+    o.allocate(mesh_moved)
+    o.prepare(mesh_moved)
+    np.testing.assert_array_equal(g["s2o"], o.maps()["s2o"])
+    assert rel_err(P2.Preconditioning(None, r), o.apply(r)) <= Z_TOL
