@@ -25,7 +25,8 @@
 // takes the row's neighbours j, j+G, ...: the 36-byte blocks of consecutive
 // rows are contiguous in the CSR, so one wave-instruction reads ~64
 // consecutive blocks; the G partial products are combined by a fixed xor
-// butterfly.  Per iteration: spmv, update_xr, apply (or copy), rz, update_p.
+// butterfly; each wave works on 4 row groups at a time so their dependent
+// load chains overlap.  Per iteration: spmv, update_xr, apply (or copy), rz, update_p.
 #include "mas_internal.h"
 
 namespace mas {
@@ -42,8 +43,12 @@ struct PcgState {
 // partial-sum slots (kPcgBlocks doubles each)
 enum { kPartPAp = 0, kPartRR = 1, kPartRZ = 2, kPartBB = 3, kParts = 4 };
 
-__device__ __forceinline__ float3 mat3_mul(const float* __restrict__ m, float4 x) {
-    // column-major 3x3: y_i = sum_j m[3 j + i] x_j
+__device__ __forceinline__ float3 mat3_mul(const float* __restrict__ src, float4 x) {
+    // column-major 3x3: y_i = sum_j m[3 j + i] x_j.  The 36-byte block is
+    // 4-byte aligned: a memcpy lets the compiler use two dwordx4 + one dword
+    // loads (unaligned-access mode) instead of nine dword loads.
+    float m[9];
+    __builtin_memcpy(m, src, 36);
     return make_float3(__fadd_rn(__fadd_rn(__fmul_rn(m[0], x.x), __fmul_rn(m[3], x.y)), __fmul_rn(m[6], x.z)),
                        __fadd_rn(__fadd_rn(__fmul_rn(m[1], x.x), __fmul_rn(m[4], x.y)), __fmul_rn(m[7], x.z)),
                        __fadd_rn(__fadd_rn(__fmul_rn(m[2], x.x), __fmul_rn(m[5], x.y)), __fmul_rn(m[8], x.z)));
@@ -55,27 +60,75 @@ __device__ __forceinline__ void add3(float3& a, float3 b) {
     a.z = __fadd_rn(a.z, b.z);
 }
 
-// (A x)[v] for the G-lane group of row v; the full sum is returned in every lane
-// of the group.  Lane j: neighbours j, j+G, ... in CSR order, lane 0 adds the
-// diagonal first; then a fixed xor butterfly over the group.
-template <int G>
-__device__ __forceinline__ float3 spmv_group(int v, bool valid, int sub, const int* __restrict__ starts,
-                                             const int* __restrict__ idx, const float* __restrict__ diag,
-                                             const float* __restrict__ off, const float4* __restrict__ x) {
-    float3 acc = make_float3(0.f, 0.f, 0.f);
-    if (valid) {
-        if (sub == 0) acc = mat3_mul(diag + 9 * (size_t)v, x[v]);
-        const int e1 = starts[v + 1];
-        for (int e = starts[v] + sub; e < e1; e += G) add3(acc, mat3_mul(off + 9 * (size_t)e, x[idx[e]]));
+// (A x)[v] for R rows per G-lane group at once (rows base + r * 64/G + lane/G):
+// every first-neighbour load of the R rows is issued before any is consumed
+// (the chain starts -> idx -> x is three dependent loads; a grid-stride loop
+// over single rows was latency-bound at 100 us for 1M rows).  Lane j takes
+// neighbours j, j+G, ... in CSR order, lane 0 adds the diagonal first; then a
+// fixed xor butterfly over the group.  The full sums are returned in every
+// lane of the group.
+template <int G, int R>
+__device__ __forceinline__ void spmv_rows(int base, int nV, int lane, const int* __restrict__ starts,
+                                          const int* __restrict__ idx, const float* __restrict__ diag,
+                                          const float* __restrict__ off, const float4* __restrict__ x,
+                                          int (&v)[R], float3 (&acc)[R]) {
+    const int sub = lane % G;
+    int e[R], e1[R], nb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        v[r] = base + r * (64 / G) + lane / G;
+        const bool valid = v[r] < nV;
+        e[r] = valid ? starts[v[r]] + sub : 0;
+        e1[r] = valid ? starts[v[r] + 1] : 0;
+    }
+    float m[R][9];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const bool has = e[r] < e1[r];
+        nb[r] = has ? idx[e[r]] : 0;
+        __builtin_memcpy(m[r], off + 9 * (size_t)(has ? e[r] : 0), 36);
+    }
+    float4 xn[R], xd[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        xn[r] = x[nb[r]];
+        xd[r] = x[v[r] < nV ? v[r] : 0];
     }
 #pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) {
-        acc.x = __fadd_rn(acc.x, __shfl_xor(acc.x, o));
-        acc.y = __fadd_rn(acc.y, __shfl_xor(acc.y, o));
-        acc.z = __fadd_rn(acc.z, __shfl_xor(acc.z, o));
+    for (int r = 0; r < R; ++r) {
+        acc[r] = make_float3(0.f, 0.f, 0.f);
+        if (sub == 0 && v[r] < nV) acc[r] = mat3_mul(diag + 9 * (size_t)v[r], xd[r]);
+        if (e[r] < e1[r]) add3(acc[r], mat3_mul(m[r], xn[r]));
+        for (int ee = e[r] + G; ee < e1[r]; ee += G) add3(acc[r], mat3_mul(off + 9 * (size_t)ee, x[idx[ee]]));
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) {
+            acc[r].x = __fadd_rn(acc[r].x, __shfl_xor(acc[r].x, o));
+            acc[r].y = __fadd_rn(acc[r].y, __shfl_xor(acc[r].y, o));
+            acc[r].z = __fadd_rn(acc[r].z, __shfl_xor(acc[r].z, o));
+        }
     }
-    return acc;
 }
+constexpr int kSpmvRows = 4;  // row groups per wave and pass
+
+// XCD-aware row ranges: workgroups are dealt round-robin over the 8 XCDs
+// (b and b + 8 share one; speed only, never correctness), so workgroups
+// b % 8 == k sweep the k-th contiguous eighth of the rows.  A row's
+// neighbours (+-1, +-W on the grid) then sit in the same XCD's L2 and the
+// x gathers stop going to the Infinity Cache.
+constexpr int kXcds = 8;
+struct XcdRows {
+    int first, end, stride;
+    __device__ __forceinline__ XcdRows(int nV, int rowsPerWave) {
+        const int xcd = blockIdx.x % kXcds, j = blockIdx.x / kXcds;
+        const int wavesPerXcd = (kPcgBlocks / kXcds) * (kPcgThreads / 64);
+        // chunks are whole row groups, so no group straddles two chunks
+        const int chunk = ((nV + kXcds - 1) / kXcds + rowsPerWave - 1) / rowsPerWave * rowsPerWave;
+        const int c0 = xcd * chunk;
+        end = min(nV, c0 + chunk);
+        first = c0 + (j * (kPcgThreads / 64) + (int)(threadIdx.x >> 6)) * rowsPerWave;
+        stride = wavesPerXcd * rowsPerWave;
+    }
+};
 
 __device__ __forceinline__ double dot3(float3 a, float4 b) {
     return (double)a.x * b.x + (double)a.y * b.y + (double)a.z * b.z;
@@ -121,17 +174,23 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_residual(int nV, const int*
                                                               const float4* __restrict__ b, float4* __restrict__ r,
                                                               double* __restrict__ part) {
     const int lane = threadIdx.x & 63, sub = lane % G;
-    const int wave = blockIdx.x * (kPcgThreads / 64) + (threadIdx.x >> 6);
+    constexpr int rowsPerWave = kSpmvRows * (64 / G);
+    XcdRows xr(nV, rowsPerWave);
     double rr = 0.0, bb = 0.0;
-    for (int base = wave * (64 / G); base < nV; base += kPcgBlocks * (kPcgThreads / 64) * (64 / G)) {
-        const int v = base + lane / G;
-        const float3 ax = spmv_group<G>(v, v < nV, sub, starts, idx, diag, off, x);
-        if (sub == 0 && v < nV) {
-            const float4 bv = b[v];
-            const float4 rv = make_float4(__fsub_rn(bv.x, ax.x), __fsub_rn(bv.y, ax.y), __fsub_rn(bv.z, ax.z), 0.f);
-            r[v] = rv;
-            rr += dot3(make_float3(rv.x, rv.y, rv.z), rv);
-            bb += dot3(make_float3(bv.x, bv.y, bv.z), bv);
+    for (int base = xr.first; base < xr.end; base += xr.stride) {
+        int v[kSpmvRows];
+        float3 ax[kSpmvRows];
+        spmv_rows<G, kSpmvRows>(base, nV, lane, starts, idx, diag, off, x, v, ax);
+#pragma unroll
+        for (int q = 0; q < kSpmvRows; ++q) {
+            if (sub == 0 && v[q] < nV) {
+                const float4 bv = b[v[q]];
+                const float4 rv = make_float4(__fsub_rn(bv.x, ax[q].x), __fsub_rn(bv.y, ax[q].y),
+                                              __fsub_rn(bv.z, ax[q].z), 0.f);
+                r[v[q]] = rv;
+                rr += dot3(make_float3(rv.x, rv.y, rv.z), rv);
+                bb += dot3(make_float3(bv.x, bv.y, bv.z), bv);
+            }
         }
     }
     block_partial(rr, part + kPartRR * kPcgBlocks);
@@ -166,14 +225,19 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __r
                                                           double* __restrict__ part) {
     if (st->done) return;
     const int lane = threadIdx.x & 63, sub = lane % G;
-    const int wave = blockIdx.x * (kPcgThreads / 64) + (threadIdx.x >> 6);
+    constexpr int rowsPerWave = kSpmvRows * (64 / G);
+    XcdRows xr(nV, rowsPerWave);
     double pap = 0.0;
-    for (int base = wave * (64 / G); base < nV; base += kPcgBlocks * (kPcgThreads / 64) * (64 / G)) {
-        const int v = base + lane / G;
-        const float3 y = spmv_group<G>(v, v < nV, sub, starts, idx, diag, off, p);
-        if (sub == 0 && v < nV) {
-            ap[v] = make_float4(y.x, y.y, y.z, 0.f);
-            pap += dot3(y, p[v]);
+    for (int base = xr.first; base < xr.end; base += xr.stride) {
+        int v[kSpmvRows];
+        float3 y[kSpmvRows];
+        spmv_rows<G, kSpmvRows>(base, nV, lane, starts, idx, diag, off, p, v, y);
+#pragma unroll
+        for (int q = 0; q < kSpmvRows; ++q) {
+            if (sub == 0 && v[q] < nV) {
+                ap[v[q]] = make_float4(y[q].x, y[q].y, y[q].z, 0.f);
+                pap += dot3(y[q], p[v[q]]);
+            }
         }
     }
     block_partial(pap, part + kPartPAp * kPcgBlocks);
