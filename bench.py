@@ -106,6 +106,11 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcg", action="store_true", help="skip the end-to-end PCG solve report")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the Morton-range sharded apply even on one GPU (overhead measurement)")
+    ap.add_argument("--graph", action="store_true",
+                    help="sharded path: replay one captured HIP graph per step (measured slower than eager "
+                         "launches on one GPU at 1M and 256k: profiles/round1/ab/shard_overhead.json)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo only to exercise N>1 on one GPU")
     args = ap.parse_args()
@@ -124,8 +129,14 @@ def main():
         local = local % ndev
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    sharded_path = world > 1 or args.sharded
+    if sharded_path:
         import torch.distributed as dist
+        if world == 1:  # a one-rank group for --sharded
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -165,10 +176,12 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    if world > 1:  # Morton-range shards + one RCCL allgather per apply
+    use_graph = False
+    if sharded_path:  # Morton-range shards + one RCCL allgather per apply
         from mas_amd.distributed import ShardedApply
         sharded = ShardedApply(P, rank, world, device=torch.device("cuda", local))
         plan = sharded.plan
+        use_graph = args.graph and args.dist_backend == "nccl"
 
         def step():
             sharded(z, r, stream)
@@ -181,6 +194,11 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if use_graph:
+        sharded.capture(z, r, stream)
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
 
     # timed region: K applies, bracketed by barrier + synchronize (no
     # instrumentation inside: per-kernel events cost ~10 us per apply).
@@ -199,6 +217,8 @@ def main():
 
     # kernel-duration pass: the same K applies with the library's HIP events
     # recorded on the apply stream around each kernel group (roofline source).
+    if use_graph:
+        sharded.graph = None  # the kernel-duration pass runs eagerly (events are recorded by the library)
     P.set_profiling(True)
     torch.cuda.synchronize()
     ev2, ev3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -256,7 +276,8 @@ def main():
             "fine_blocks": info["num_fine_blocks"],
             "contact_stencils": info["num_stencils"],
             "parallelism": (f"{world} Morton-range shards, {args.dist_backend} allgather of level-1 segments"
-                            if world > 1 else "single-gpu"),
+                            + (", HIP-graph replay" if use_graph else ", eager launches")
+                            if sharded_path else "single-gpu"),
         },
         "roofline": {
             "bound": "hbm",
