@@ -88,7 +88,10 @@ typedef struct {
     double apply_ms_avg;       /* apply start -> apply end on the caller stream */
     double pre_fine_ms_avg;    /* before the fine kernel: coarse chain (serial mode) or fork (overlap mode) */
     double fine_ms_avg;        /* the fine-level kernel: gather + level-0 block solves (+ prolongation) -- dominant */
-    double post_fine_ms_avg;   /* after it: join with the coarse chain + prolongation pass (overlap mode) */
+    double post_fine_ms_avg;   /* after it: join with the coarse chain + prolongation pass (overlap mode),
+                                  */
+    int64_t apply_mode;        /* 1: coarse levels in one launch (k_coarse_chain), 0: one launch per
+                                  coarse level, 2: side-stream overlap */
 } mas_stats;
 
 /* lifecycle */

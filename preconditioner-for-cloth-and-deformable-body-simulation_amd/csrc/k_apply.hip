@@ -317,7 +317,10 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
         launch_prolong(h, 0, h->nV, d_z, s);
         if (ev) hipEventRecord(ev[3], s);
     } else {
-        if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
+        // coarse levels: one launch climbing by last arrival
+        // (k_coarse_chain.hip), or one launch per level; bitwise equal
+        if (h->L > 1 && h->chain) launch_coarse_chain(h, d_r, s);
+        else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
         if (ev) hipEventRecord(ev[1], s);
         launch_fine(h, 0, h->nFineBlk, d_r, d_z, s);
         if (ev) hipEventRecord(ev[2], s);
@@ -349,7 +352,8 @@ int build_l1src(mas_context* h, hipStream_t s) {
     if (rc) return rc;
     k_l1src<<<cdiv((long long)n1Pad * 32, 256), 256, 0, s>>>(n1Pad, n1, P<int2>(h->members), P<int>(h->s2o),
                                                              P<int>(h->l1src));
-    return hip_check(h, hipGetLastError(), "l1src");
+    if ((rc = hip_check(h, hipGetLastError(), "l1src"))) return rc;
+    return build_chain_tables(h, s);
 }
 
 // Apply-side tables, built once per Prepare: members[] for every coarse node,

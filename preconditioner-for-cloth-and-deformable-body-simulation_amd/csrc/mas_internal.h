@@ -62,6 +62,7 @@ struct mas_context {
     hipStream_t stream2 = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;
     int factorVariant = 2;  // 2 = register-blocked k_factor_rb; env MAS_FACTOR_VARIANT=0: LDS-row k_factor
+    int chain = 0;        // 1 = coarse levels in one launch (k_coarse_chain.hip, env MAS_COARSE_CHAIN=1); measured 24.4 vs 22.7 us for one launch per level at 1M
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     int levelSize[2 * 9] = {};
@@ -79,6 +80,7 @@ struct mas_context {
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, l1src;
+    mas::Buffer chainPrange, chainNeed, chainCnt;  // one-launch coarse chain (k_coarse_chain.hip)
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     std::vector<int> l1First;  // first level-1 local id per level-0 bank (+ n1), for sharding
     int shardWorld = 0;
@@ -100,7 +102,7 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &l1src, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -134,6 +136,8 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s);
 int upload_slot_table(mas_context* h);
 int prepare_apply_tables(mas_context* h, hipStream_t s);
 int build_l1src(mas_context* h, hipStream_t s);
+int build_chain_tables(mas_context* h, hipStream_t s);
+void launch_coarse_chain(mas_context* h, const float4* r, hipStream_t s);
 int compute_l1_first(mas_context* h, hipStream_t s);
 int copy_block_inverse(mas_context* h, int blk, float* out96);
 int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,

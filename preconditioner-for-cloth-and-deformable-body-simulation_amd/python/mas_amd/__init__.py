@@ -53,7 +53,8 @@ class mas_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in ("allocate_ms", "prepare_ms", "prepare_levels_ms",
                                                "prepare_assemble_ms", "prepare_factor_ms")] + \
                [("apply_calls", ctypes.c_int64), ("profiled_applies", ctypes.c_int64)] + \
-               [(n, ctypes.c_double) for n in ("apply_ms_avg", "pre_fine_ms_avg", "fine_ms_avg", "post_fine_ms_avg")]
+               [(n, ctypes.c_double) for n in ("apply_ms_avg", "pre_fine_ms_avg", "fine_ms_avg", "post_fine_ms_avg")] + \
+               [("apply_mode", ctypes.c_int64)]
 
 
 class mas_shard(ctypes.Structure):
