@@ -232,10 +232,22 @@ def main():
     P.set_profiling(False)
 
     t_max = elapsed
+    shard_check = None
     if dist is not None:
         tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
+        # correctness of the sharded path on this run: every rank's own z
+        # entries must equal the unsharded apply's bitwise (no communication
+        # needed: each rank checks its own slice, then one MIN over ranks)
+        z_ref = torch.zeros_like(r)
+        P.PreconditioningDevice(z_ref, r, sptr)
+        torch.cuda.synchronize()
+        own = torch.from_numpy(P.maps()["s2o"][plan["vert_begin"]:plan["vert_end"]].astype(np.int64)).cuda()
+        ok = torch.tensor([1.0 if torch.equal(z[own], z_ref[own]) else 0.0], device="cuda", dtype=torch.float64)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        shard_check = {"own_slices_bitwise_equal_unsharded": bool(ok.item() == 1.0),
+                       "form": "overlapped (fine during allgather)" if sharded.overlap else "serial"}
 
     fine_bytes, apply_bytes = algorithmic_bytes(info)
     if plan is not None:  # the rank's own level-0 blocks and vertices
@@ -313,6 +325,8 @@ def main():
         "wall_s_timed": round(wall, 4),
         "cpu_baseline": None,
     }
+    if shard_check is not None:
+        out["shard_check"] = shard_check
 
     if rank == 0 and world == 1 and not args.no_pcg:
         # end-to-end context (not the metric): one GPU-resident PCG solve of

@@ -181,6 +181,16 @@ int mas_shard_setup(mas_handle h, int rank, int world, mas_shard* out);
 int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r4, float* d_seg4, void* stream);
 int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gathered4, const float* d_r4,
                            float* d_z4, void* stream);
+/* Overlapped form of step 3.  The level-0 block solves need no
+ * exchanged data, so they can run while the allgather is in flight:
+ *   3a. mas_apply_shard_fine: own level-0 blocks, z = Z0 for own vertices (no
+ *       coarse terms); enqueue it right after the allgather is started;
+ *   3b. mas_apply_shard_complete (after the allgather): the coarse levels from
+ *       d_gathered, then z += Z1 + Z2 + Z3 for own vertices (CollectFinalZ order).
+ * 3a then 3b is bitwise equal to mas_apply_shard_finish. */
+int mas_apply_shard_fine(mas_handle h, int rank, int world, const float* d_r4, float* d_z4, void* stream);
+int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_gathered4, float* d_z4,
+                             void* stream);
 
 /* ---- fixture / wire format ----
  * A prepared handle as one versioned, checksummed blob (header "MASBLOB",

@@ -6,10 +6,14 @@
 // l1_first[fb1]).  Per apply and rank:
 //   k_restrict_seg   R1 of the own segment (same ordered sums as k_coarse_l1)
 //   -- caller: allgather of the padded segments over RCCL --
-//   k_unpack_r1      gathered segments -> R1 of every level-1 node
-//   k_solve_nodes    own level-1 blocks: Z1 = Inv R1
-//   k_coarse_up      every block of levels >= 2 (tiny, redundant on all ranks)
+//   k_shard_coarse12 own level-1 blocks (Z1 = Inv R1) and every level-2 block
+//                    (R2 from the gathered R1, Z2), straight from the
+//                    gathered segments, one launch
+//   k_coarse_up      every block of levels >= 3 (tiny, redundant on all ranks)
 //   k_solve_fine     own level-0 blocks + prolongation, z of own vertices
+// or, overlapped (mas_apply_shard_fine / _complete): k_solve_fine without the
+// coarse terms while the allgather is in flight, then the coarse kernels and
+// k_prolong over the own vertices.
 // Every value is computed by the same kernel arithmetic as the unsharded
 // apply, so the union of the ranks' outputs is bitwise equal to it.
 #include <algorithm>
@@ -20,18 +24,21 @@
 namespace mas {
 
 void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s);
+void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s);
+void launch_prolong(mas_context* h, int v0, int v1, float4* z, hipStream_t s);
 void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
 
-__global__ __launch_bounds__(256) void k_restrict_seg(int l1Begin, int count, int segMax,
-                                                      const int2* __restrict__ members, const int* __restrict__ s2o,
+// R1 of the own level-1 segment, one thread per node: the children's
+// original ids come from l1src (32 per node, -1 where none, built at Prepare),
+// so the r gather is the second dependent load; summed in lane order from +0
+// as k_coarse_l1.
+__global__ __launch_bounds__(256) void k_restrict_seg(int l1Begin, int count, int segMax, const int* __restrict__ l1src,
                                                       const float4* __restrict__ r, float4* __restrict__ seg) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= segMax) return;
     float ax = 0.f, ay = 0.f, az = 0.f;
     if (i < count) {
-        const int2 mb = members[l1Begin + i];  // level-1 local id == coarse index
-        const unsigned msk = (unsigned)mb.y;
-        const int4* s4 = reinterpret_cast<const int4*>(s2o + mb.x * 32);
+        const int4* s4 = reinterpret_cast<const int4*>(l1src + (size_t)(l1Begin + i) * 32);
         int src[32];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -44,15 +51,14 @@ __global__ __launch_bounds__(256) void k_restrict_seg(int l1Begin, int count, in
         float vx[32], vy[32], vz[32];
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if ((msk >> j) & 1u) v = r[src[j]];
+            const float4 v = r[src[j] >= 0 ? src[j] : 0];
             vx[j] = v.x;
             vy[j] = v.y;
             vz[j] = v.z;
         }
 #pragma unroll
         for (int j = 0; j < 32; ++j)
-            if ((msk >> j) & 1u) {
+            if (src[j] >= 0) {
                 ax = __fadd_rn(ax, vx[j]);
                 ay = __fadd_rn(ay, vy[j]);
                 az = __fadd_rn(az, vz[j]);
@@ -61,28 +67,85 @@ __global__ __launch_bounds__(256) void k_restrict_seg(int l1Begin, int count, in
     seg[i] = make_float4(ax, ay, az, 0.f);
 }
 
-__global__ __launch_bounds__(256) void k_unpack_r1(int segMax, int world, const int* __restrict__ off,
-                                                   const float4* __restrict__ gathered, float4* __restrict__ rc) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= segMax * world) return;
-    const int rk = t / segMax, i = t % segMax;
-    if (i < off[rk + 1] - off[rk]) rc[off[rk] + i] = gathered[t];
+// pos1[i] = index of level-1 node i's R1 in the gathered buffer
+// (g * segMax + i - off[g] for the rank g whose segment holds i); rebuilt when
+// the world size changes.
+__global__ __launch_bounds__(256) void k_shard_pos1(int n1, int world, int segMax, const int* __restrict__ off,
+                                                    int* __restrict__ pos1) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n1) return;
+    int lo = 0, hi = world;  // largest g with off[g] <= i (skips empty segments)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (off[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    pos1[i] = lo * segMax + (i - off[lo]);
 }
 
-// Z = Inv R for blocks [blk0, blk0 + nb) whose R is already in Rc.
-__global__ __launch_bounds__(kApplyThreads) void k_solve_nodes(const float4* __restrict__ inv, int blk0, int nb,
-                                                              const float4* __restrict__ rc, float4* __restrict__ zc,
-                                                              int begin1) {
+// Levels 1 and 2 of a sharded apply in ONE launch, straight from the gathered
+// segments (no unpack pass): waves [0, nOwn1) solve the rank's own level-1
+// blocks (Z1 = Inv R1), waves [nOwn1, nOwn1 + nb2) compute R2 of every level-2
+// block -- each node sums its children's R1 in child-lane order from +0, as
+// k_coarse_up -- and solve it.  Both only read the gathered R1, so they are
+// independent; levels >= 3 follow as k_coarse_up launches.  Replaces unpack +
+// own level-1 solve + level-2 launch (three latency-bound launches).
+__global__ __launch_bounds__(kApplyThreads) void k_shard_coarse12(
+    const float4* __restrict__ inv, const float4* __restrict__ gathered, const int* __restrict__ pos1, int own1Blk0,
+    int nOwn1, int n1, int lv2Blk0, int nb2, int n2, const int2* __restrict__ members, int begin1,
+    float4* __restrict__ rc, float4* __restrict__ zc) {
     const int lane = threadIdx.x & 63, n = lane & 31;
     const int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
-    if (w >= nb) return;
-    const int blk = blk0 + w;
-    const int node = blk * 32 + n - begin1;
+    if (w >= nOwn1 + nb2) return;  // wave-uniform
+    const bool l1 = w < nOwn1;
+    const int blk = l1 ? own1Blk0 + w : lv2Blk0 + (w - nOwn1);
+    const int node = blk * 32 + n;
     float g[kRecord], tl[3];
     load_record<true>(inv, blk, lane, g, tl);
-    const float4 rr = rc[node];
-    const float3 out = block_solve(g, tl, make_float3(rr.x, rr.y, rr.z), lane);
-    if (lane < 32) zc[node] = make_float4(out.x, out.y, out.z, 0.f);
+    float ax = 0.f, ay = 0.f, az = 0.f;
+    if (l1) {
+        const int i = node - begin1;
+        if (lane < 32 && i < n1) {
+            const float4 v = gathered[pos1[i]];
+            ax = v.x; ay = v.y; az = v.z;
+        }
+    } else if (lane < 32 && node - lv2Blk0 * 32 < n2) {
+        const int2 mb = members[node - begin1];
+        const unsigned msk = (unsigned)mb.y;
+        const int4* p4 = reinterpret_cast<const int4*>(pos1 + mb.x * 32);  // the child bank's 32 level-1 ids
+        int src[32];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int4 t = p4[q];
+            src[4 * q] = t.x;
+            src[4 * q + 1] = t.y;
+            src[4 * q + 2] = t.z;
+            src[4 * q + 3] = t.w;
+        }
+        float vx[32], vy[32], vz[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const float4 v = gathered[(msk >> j) & 1u ? src[j] : 0];
+            vx[j] = v.x; vy[j] = v.y; vz[j] = v.z;
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((msk >> j) & 1u) {
+                ax = __fadd_rn(ax, vx[j]);
+                ay = __fadd_rn(ay, vy[j]);
+                az = __fadd_rn(az, vz[j]);
+            }
+        }
+    }
+    // half 1 takes node n's residual from lane n
+    ax = __shfl(ax, n);
+    ay = __shfl(ay, n);
+    az = __shfl(az, n);
+    const float3 out = block_solve(g, tl, make_float3(ax, ay, az), lane);
+    if (lane < 32) {
+        rc[node - begin1] = make_float4(ax, ay, az, 0.f);
+        zc[node - begin1] = make_float4(out.x, out.y, out.z, 0.f);
+    }
 }
 
 int compute_l1_first(mas_context* h, hipStream_t s) {
@@ -142,10 +205,45 @@ int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     if (h->L < 2) return hip_check(h, hipMemsetAsync(d_seg4, 0, (size_t)sh.seg_max * 16, s), "zero segment");
     k_restrict_seg<<<cdiv(sh.seg_max, 256), 256, 0, s>>>(sh.l1_begin, sh.l1_end - sh.l1_begin, sh.seg_max,
-                                                         P<int2>(h->members), P<int>(h->s2o),
-                                                         reinterpret_cast<const float4*>(d_r4),
+                                                         P<int>(h->l1src), reinterpret_cast<const float4*>(d_r4),
                                                          reinterpret_cast<float4*>(d_seg4));
     return hip_check(h, hipGetLastError(), "shard restrict");
+}
+
+// The coarse levels of a sharded apply from the gathered level-1 segments:
+// R1 of every level-1 node, Z1 of the own level-1 blocks, every block of
+// levels >= 2.
+static int shard_coarse(mas_context* h, const mas_shard& sh, int world, const float* d_gathered4, hipStream_t s) {
+    int rc;
+    const int n1 = h->levelSize[2];
+    if (h->shardWorld != world) {  // per-rank segment offsets (level-1 local ids) -> pos1
+        std::vector<int> off(world + 1);
+        for (int g = 0; g <= world; ++g) off[g] = h->l1First[(int)((long long)g * h->nFineBlk / world)];
+        if ((rc = ensure(h, h->shardOff, (size_t)(world + 1) * 4)) ||
+            (rc = ensure(h, h->shardPos1, (size_t)ceil32(n1) * 4)) ||
+            (rc = hip_check(h, hipMemcpy(h->shardOff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice),
+                            "H2D shard offsets")) ||
+            (rc = hip_check(h, hipMemsetAsync(h->shardPos1.p, 0, (size_t)ceil32(n1) * 4, s), "memset pos1")))
+            return rc;
+        k_shard_pos1<<<cdiv(n1, 256), 256, 0, s>>>(n1, world, sh.seg_max, P<int>(h->shardOff), P<int>(h->shardPos1));
+        h->shardWorld = world;
+    }
+    const int begin1 = h->levelSize[3];
+    const int own0 = sh.l1_end > sh.l1_begin ? sh.l1_begin / 32 : 0;
+    const int nOwn1 = sh.l1_end > sh.l1_begin ? (sh.l1_end + 31) / 32 - own0 : 0;
+    const int nb2 = h->L > 2 ? ceil32(h->levelSize[4]) / 32 : 0;
+    const int n2 = h->L > 2 ? h->levelSize[4] : 0;
+    const int lv2Blk0 = h->L > 2 ? h->levelSize[5] / 32 : 0;
+    if (nOwn1 + nb2 > 0)
+        k_shard_coarse12<<<cdiv(nOwn1 + nb2, kApplyThreads / 64), kApplyThreads, 0, s>>>(
+            P<float4>(h->inv), reinterpret_cast<const float4*>(d_gathered4), P<int>(h->shardPos1), begin1 / 32 + own0,
+            nOwn1, n1, lv2Blk0, nb2, n2, P<int2>(h->members), begin1, P<float4>(h->Rc), P<float4>(h->Zc));
+    launch_coarse_levels(h, 3, nullptr, s);
+    return MAS_OK;
+}
+
+static hipEvent_t* shard_events(mas_context* h) {
+    return h->profiling && h->profRecorded < kProfRing ? &h->prof[4 * h->profRecorded++] : nullptr;
 }
 
 int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gathered4, const float* d_r4,
@@ -158,35 +256,55 @@ int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gat
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     const float4* r = reinterpret_cast<const float4*>(d_r4);
     float4* z = reinterpret_cast<float4*>(d_z4);
-    hipEvent_t* ev = nullptr;
-    if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
+    hipEvent_t* ev = shard_events(h);
     if (ev) hipEventRecord(ev[0], s);
-    if (h->L > 1) {
-        if (h->shardWorld != world) {  // per-rank segment offsets (level-1 local ids)
-            std::vector<int> off(world + 1);
-            for (int g = 0; g <= world; ++g) off[g] = h->l1First[(int)((long long)g * h->nFineBlk / world)];
-            if ((rc = ensure(h, h->shardOff, (size_t)(world + 1) * 4)) ||
-                (rc = hip_check(h, hipMemcpy(h->shardOff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice),
-                                "H2D shard offsets")))
-                return rc;
-            h->shardWorld = world;
-        }
-        const int begin1 = h->levelSize[3];
-        k_unpack_r1<<<cdiv((long long)sh.seg_max * world, 256), 256, 0, s>>>(
-            sh.seg_max, world, P<int>(h->shardOff), reinterpret_cast<const float4*>(d_gathered4), P<float4>(h->Rc));
-        if (sh.l1_end > sh.l1_begin) {
-            const int b0 = sh.l1_begin / 32, b1 = (sh.l1_end + 31) / 32;
-            k_solve_nodes<<<cdiv(b1 - b0, kApplyThreads / 64), kApplyThreads, 0, s>>>(
-                P<float4>(h->inv), begin1 / 32 + b0, b1 - b0, P<float4>(h->Rc), P<float4>(h->Zc), begin1);
-        }
-        launch_coarse_levels(h, 2, r, s);
-    }
+    if (h->L > 1 && (rc = shard_coarse(h, sh, world, d_gathered4, s))) return rc;
     if (ev) hipEventRecord(ev[1], s);
     launch_fine(h, sh.fine_block_begin, sh.fine_block_end, r, z, s);
     if (ev) hipEventRecord(ev[2], s);
     if (ev) hipEventRecord(ev[3], s);
     h->stats.apply_calls++;
     return hip_check(h, hipGetLastError(), "shard finish");
+}
+
+// Profiling events of the overlapped form: [0] = [1] before the level-0
+// kernel (fine), [2] after it, [3] after complete (allgather wait + coarse +
+// prolongation), so fine_ms_avg is the level-0 kernel as in the other forms.
+int mas_apply_shard_fine(mas_handle h, int rank, int world, const float* d_r4, float* d_z4, void* stream) {
+    if (!h || !d_r4 || !d_z4) return MAS_ERR_ARG;
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    mas_shard sh;
+    int rc = mas_shard_setup(h, rank, world, &sh);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    hipEvent_t* ev = shard_events(h);
+    h->shardPendingEv = ev;
+    if (ev) {
+        hipEventRecord(ev[0], s);
+        hipEventRecord(ev[1], s);
+    }
+    launch_fine_z0(h, sh.fine_block_begin, sh.fine_block_end, reinterpret_cast<const float4*>(d_r4),
+                   reinterpret_cast<float4*>(d_z4), s);
+    if (ev) hipEventRecord(ev[2], s);
+    return hip_check(h, hipGetLastError(), "shard fine");
+}
+
+int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_gathered4, float* d_z4,
+                             void* stream) {
+    if (!h || !d_gathered4 || !d_z4) return MAS_ERR_ARG;
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    mas_shard sh;
+    int rc = mas_shard_setup(h, rank, world, &sh);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    if (h->L > 1) {
+        if ((rc = shard_coarse(h, sh, world, d_gathered4, s))) return rc;
+        launch_prolong(h, sh.vert_begin, sh.vert_end, reinterpret_cast<float4*>(d_z4), s);
+    }
+    if (h->shardPendingEv) hipEventRecord(h->shardPendingEv[3], s);
+    h->shardPendingEv = nullptr;
+    h->stats.apply_calls++;
+    return hip_check(h, hipGetLastError(), "shard complete");
 }
 
 }  // extern "C"

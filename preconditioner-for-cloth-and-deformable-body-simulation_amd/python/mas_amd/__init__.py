@@ -33,6 +33,7 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
            "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_get_info",
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
            "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
+           "mas_apply_shard_fine", "mas_apply_shard_complete",
            "mas_pcg_solve_device", "mas_pcg_solve", "mas_blob_size", "mas_save_blob", "mas_load_blob"]
 
 
@@ -116,6 +117,8 @@ def lib():
         L.mas_shard_setup.argtypes = [P, I, I, ctypes.POINTER(mas_shard)]
         L.mas_apply_shard_restrict.argtypes = [P, I, I, P, P, P]
         L.mas_apply_shard_finish.argtypes = [P, I, I, P, P, P, P]
+        L.mas_apply_shard_fine.argtypes = [P, I, I, P, P, P]
+        L.mas_apply_shard_complete.argtypes = [P, I, I, P, P, P]
         F = ctypes.c_float
         L.mas_pcg_solve_device.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result), P]
         L.mas_pcg_solve.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result)]
@@ -225,6 +228,15 @@ class SeSchwarzPreconditioner:
     def shard_finish(self, rank, world, gathered, r, z, stream=None):
         self._check(self._L.mas_apply_shard_finish(self.h, rank, world, _ptr(gathered), _ptr(r), _ptr(z),
                                                    _ptr(stream)), "shard_finish")
+
+    def shard_fine(self, rank, world, r, z, stream=None):
+        """Overlapped step 3a: own level-0 blocks, z = Z0 (no coarse terms)."""
+        self._check(self._L.mas_apply_shard_fine(self.h, rank, world, _ptr(r), _ptr(z), _ptr(stream)), "shard_fine")
+
+    def shard_complete(self, rank, world, gathered, z, stream=None):
+        """Overlapped step 3b: coarse levels from the gathered segments, z += prolongation."""
+        self._check(self._L.mas_apply_shard_complete(self.h, rank, world, _ptr(gathered), _ptr(z), _ptr(stream)),
+                    "shard_complete")
 
     # ---- GPU-resident PCG (include/mas_capi.h, SURVEY 8(f) 1) ----
     def pcg_solve(self, diagonal, csrOffDiagonals, csrRanges, b, x0=None, max_iters=1000, tol=1e-5,

@@ -10,7 +10,7 @@ from conftest import cloth, tet
 pytestmark = pytest.mark.gpu
 
 
-def _virtual_sharded(P, r, world):
+def _virtual_sharded(P, r, world, overlap=False):
     import torch
     plans = [P.shard_setup(g, world) for g in range(world)]
     seg = plans[0]["seg_max"]
@@ -23,7 +23,11 @@ def _virtual_sharded(P, r, world):
         gathered = torch.cat(segs, 0).contiguous()
         z = torch.full_like(r, float("nan"))
         for g in range(world):
-            P.shard_finish(g, world, gathered, r, z, s.cuda_stream)
+            if overlap:  # level-0 blocks first (z = Z0), then coarse + prolongation
+                P.shard_fine(g, world, r, z, s.cuda_stream)
+                P.shard_complete(g, world, gathered, z, s.cuda_stream)
+            else:
+                P.shard_finish(g, world, gathered, r, z, s.cuda_stream)
     s.synchronize()
     # ranges tile the vertices exactly
     assert plans[0]["vert_begin"] == 0 and plans[-1]["vert_end"] == r.shape[0]
@@ -47,8 +51,9 @@ def test_virtual_shards_bitwise(kind, W, L, worlds):
     P.PreconditioningDevice(z_ref, r, s.cuda_stream)
     s.synchronize()
     for world in worlds:
-        z = _virtual_sharded(P, r, world)
-        assert torch.equal(z, z_ref), (world, float((z - z_ref).abs().max()))
+        for overlap in (False, True):
+            z = _virtual_sharded(P, r, world, overlap)
+            assert torch.equal(z, z_ref), (world, overlap, float((z - z_ref).abs().max()))
 
 
 def test_sharded_apply_helper_world1():
@@ -66,3 +71,22 @@ def test_sharded_apply_helper_world1():
     S(z, r, s)
     s.synchronize()
     assert np.array_equal(z.cpu().numpy(), P.Preconditioning(None, r.cpu().numpy()))
+
+
+def test_sharded_apply_helper_overlap_world1():
+    """The overlapped helper path (fine, then complete) on a one-rank world."""
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    from mas_amd.distributed import ShardedApply
+    mesh = cloth(100)
+    P = mas_amd.from_mesh(mesh, max_levels=3)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 9)).cuda()
+    z = torch.zeros_like(r)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    for overlap in (True, False):
+        S = ShardedApply(P, 0, 1, overlap=overlap)
+        S(z, r, s)
+        s.synchronize()
+        assert np.array_equal(z.cpu().numpy(), P.Preconditioning(None, r.cpu().numpy())), overlap
