@@ -90,8 +90,9 @@ typedef struct {
     double fine_ms_avg;        /* the fine-level kernel: gather + level-0 block solves (+ prolongation) -- dominant */
     double post_fine_ms_avg;   /* after it: join with the coarse chain + prolongation pass (overlap mode),
                                   */
-    int64_t apply_mode;        /* 1: coarse levels in one launch (k_coarse_chain), 0: one launch per
-                                  coarse level, 2: side-stream overlap */
+    int64_t apply_mode;        /* coarse levels: 2 = restrictions then all solves, two launches
+                                  (default); 1 = one launch (k_coarse_chain); 0 = one launch per level;
+                                  3 = side-stream overlap */
 } mas_stats;
 
 /* lifecycle */

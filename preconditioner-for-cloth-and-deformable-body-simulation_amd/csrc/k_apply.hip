@@ -317,9 +317,9 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
         launch_prolong(h, 0, h->nV, d_z, s);
         if (ev) hipEventRecord(ev[3], s);
     } else {
-        // coarse levels: one launch climbing by last arrival
-        // (k_coarse_chain.hip), or one launch per level; bitwise equal
-        if (h->L > 1 && h->chain) launch_coarse_chain(h, d_r, s);
+        // coarse levels (mas_internal.h coarseMode); all forms bitwise equal
+        if (h->L > 2 && h->coarseMode == 2) launch_coarse_twopass(h, d_r, s);
+        else if (h->L > 1 && h->coarseMode == 1) launch_coarse_chain(h, d_r, s);
         else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
         if (ev) hipEventRecord(ev[1], s);
         launch_fine(h, 0, h->nFineBlk, d_r, d_z, s);

@@ -92,7 +92,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_OVERLAP")) h->overlap = std::atoi(v);
-    if (const char* v = std::getenv("MAS_COARSE_CHAIN")) h->chain = std::atoi(v);
+    if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
     // Side stream of the MAS_OVERLAP=1 variant (off by default): highest
     // priority unless MAS_SIDE_PRIORITY=0.  Streams do run kernels
     // concurrently on MI355X (scripts/dev/stream_overlap.hip), but the level-2
@@ -318,7 +318,7 @@ int mas_get_stats(mas_handle h, mas_stats* out) {
         h->stats.fine_ms_avg = sf / n;
         h->stats.post_fine_ms_avg = sc / n;
     }
-    h->stats.apply_mode = h->overlap ? 2 : h->chain ? 1 : 0;
+    h->stats.apply_mode = h->overlap ? 3 : h->coarseMode;
     *out = h->stats;
     return MAS_OK;
 }

@@ -62,7 +62,10 @@ struct mas_context {
     hipStream_t stream2 = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;
     int factorVariant = 2;  // 2 = register-blocked k_factor_rb; env MAS_FACTOR_VARIANT=0: LDS-row k_factor
-    int chain = 0;        // 1 = coarse levels in one launch (k_coarse_chain.hip, env MAS_COARSE_CHAIN=1); measured 24.4 vs 22.7 us for one launch per level at 1M
+    // coarse levels (env MAS_COARSE_MODE): 2 = two launches, restrictions then all
+    // solves (k_coarse_twopass.hip, L >= 3); 1 = one launch climbing by last
+    // arrival (k_coarse_chain.hip; 24.4 vs 22.7 us per level at 1M); 0 = one launch per level
+    int coarseMode = 2;
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     int levelSize[2 * 9] = {};
@@ -139,6 +142,7 @@ int prepare_apply_tables(mas_context* h, hipStream_t s);
 int build_l1src(mas_context* h, hipStream_t s);
 int build_chain_tables(mas_context* h, hipStream_t s);
 void launch_coarse_chain(mas_context* h, const float4* r, hipStream_t s);
+void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s);
 int compute_l1_first(mas_context* h, hipStream_t s);
 int copy_block_inverse(mas_context* h, int blk, float* out96);
 int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,

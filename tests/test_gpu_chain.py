@@ -1,5 +1,6 @@
-"""The one-launch coarse chain (k_coarse_chain.hip) against one launch per
-coarse level (k_apply.hip).
+"""The coarse-level launch forms against one launch per coarse level
+(k_apply.hip): the one-launch chain (k_coarse_chain.hip) and the two-pass form
+(k_coarse_twopass.hip, the default).
 
 The chain kernel hands coarse residuals/solutions between workgroups inside
 one launch (write-through sc1 stores, agent-scope arrival counters that reset
@@ -17,14 +18,15 @@ from conftest import cloth, tet
 pytestmark = pytest.mark.gpu
 
 
-def _pair(mesh, L, contacts, monkeypatch):
+def _handles(mesh, L, contacts, monkeypatch):
+    """Per-level (mode 0), one-launch chain (1), two-pass (2) handles."""
     import mas_amd
-    monkeypatch.setenv("MAS_COARSE_CHAIN", "0")
-    P3 = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
-    monkeypatch.setenv("MAS_COARSE_CHAIN", "1")
-    PF = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
-    assert P3.stats()["apply_mode"] == 0 and PF.stats()["apply_mode"] == 1
-    return P3, PF
+    hs = []
+    for mode in (0, 1, 2):
+        monkeypatch.setenv("MAS_COARSE_MODE", str(mode))
+        hs.append(mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts))
+        assert hs[-1].stats()["apply_mode"] == mode
+    return hs
 
 
 def _applies(P, rs, stream):
@@ -48,17 +50,18 @@ def test_chain_equals_per_level(kind, W, L, nc, monkeypatch):
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=11) if nc else None
-    P3, PF = _pair(mesh, L, contacts, monkeypatch)
+    P3, PF, P2 = _handles(mesh, L, contacts, monkeypatch)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 100 + k)).cuda() for k in range(24)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    zf = _applies(PF, rs, s)
-    for k, (a, b) in enumerate(zip(zf, z3)):
-        np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
-    # and again on the same handle (the arrival counters reset themselves)
-    zf2 = _applies(PF, rs[::-1], s)
-    for k, (a, b) in enumerate(zip(zf2, z3[::-1])):
-        np.testing.assert_array_equal(a, b, err_msg=f"second pass, apply {k}")
+    for PX in (PF, P2):
+        zf = _applies(PX, rs, s)
+        for k, (a, b) in enumerate(zip(zf, z3)):
+            np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
+        # and again on the same handle (the chain's arrival counters reset themselves)
+        zf2 = _applies(PX, rs[::-1], s)
+        for k, (a, b) in enumerate(zip(zf2, z3[::-1])):
+            np.testing.assert_array_equal(a, b, err_msg=f"second pass, apply {k}")
 
 
 def test_chain_1m_contacts_bitwise_and_oracle(monkeypatch):
@@ -69,13 +72,14 @@ def test_chain_1m_contacts_bitwise_and_oracle(monkeypatch):
     from oracle import Oracle
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    P3, PF = _pair(mesh, 4, contacts, monkeypatch)
+    P3, PF, P2 = _handles(mesh, 4, contacts, monkeypatch)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 0x5EED + k)).cuda() for k in range(40)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    zf = _applies(PF, rs, s)
-    for k, (a, b) in enumerate(zip(zf, z3)):
-        np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
+    for PX in (PF, P2):
+        zf = _applies(PX, rs, s)
+        for k, (a, b) in enumerate(zip(zf, z3)):
+            np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
     o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], 4, 8)
     o.allocate(mesh)
     o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
@@ -91,10 +95,10 @@ def test_chain_interleaved_handles(monkeypatch):
     from mas_amd import meshgen
     ma, mb = cloth(64), tet(12)
     import mas_amd
-    monkeypatch.setenv("MAS_COARSE_CHAIN", "1")
+    monkeypatch.setenv("MAS_COARSE_MODE", "1")
     A = mas_amd.from_mesh(ma, max_levels=3)
     B = mas_amd.from_mesh(mb, max_levels=3)
-    monkeypatch.setenv("MAS_COARSE_CHAIN", "0")
+    monkeypatch.setenv("MAS_COARSE_MODE", "0")
     A3 = mas_amd.from_mesh(ma, max_levels=3)
     B3 = mas_amd.from_mesh(mb, max_levels=3)
     s = torch.cuda.Stream()
