@@ -353,7 +353,7 @@ int build_l1src(mas_context* h, hipStream_t s) {
     k_l1src<<<cdiv((long long)n1Pad * 32, 256), 256, 0, s>>>(n1Pad, n1, P<int2>(h->members), P<int>(h->s2o),
                                                              P<int>(h->l1src));
     if ((rc = hip_check(h, hipGetLastError(), "l1src"))) return rc;
-    return build_chain_tables(h, s);
+    return h->coarseMode == 1 ? build_chain_tables(h, s) : MAS_OK;
 }
 
 // Apply-side tables, built once per Prepare: members[] for every coarse node,
