@@ -32,7 +32,7 @@ void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStre
 // original ids come from l1src (32 per node, -1 where none, built at Prepare),
 // so the r gather is the second dependent load; summed in lane order from +0
 // as k_coarse_l1.
-__global__ __launch_bounds__(256) void k_restrict_seg(int l1Begin, int count, int segMax, const int* __restrict__ l1src,
+__global__ __launch_bounds__(64) void k_restrict_seg(int l1Begin, int count, int segMax, const int* __restrict__ l1src,
                                                       const float4* __restrict__ r, float4* __restrict__ seg) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= segMax) return;
@@ -204,7 +204,7 @@ int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     if (h->L < 2) return hip_check(h, hipMemsetAsync(d_seg4, 0, (size_t)sh.seg_max * 16, s), "zero segment");
-    k_restrict_seg<<<cdiv(sh.seg_max, 256), 256, 0, s>>>(sh.l1_begin, sh.l1_end - sh.l1_begin, sh.seg_max,
+    k_restrict_seg<<<cdiv(sh.seg_max, 64), 64, 0, s>>>(sh.l1_begin, sh.l1_end - sh.l1_begin, sh.seg_max,
                                                          P<int>(h->l1src), reinterpret_cast<const float4*>(d_r4),
                                                          reinterpret_cast<float4*>(d_seg4));
     return hip_check(h, hipGetLastError(), "shard restrict");
