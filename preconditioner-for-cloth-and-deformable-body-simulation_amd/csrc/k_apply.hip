@@ -1,6 +1,10 @@
 // k_apply.hip -- Preconditioning (.cpp:100-110, 1548-1719): the hot path.
 //
-// Per apply, L launches on one stream:
+// Per apply, on one stream: the coarse levels, then k_solve_fine.  For
+// L >= 3 the coarse levels default to two launches (k_coarse_twopass.hip:
+// all restrictions, then all solves); the per-level form below is kept as
+// coarseMode 0 (and is the L = 2 path), the one-launch chain as mode 1
+// (k_coarse_chain.hip).  All forms are bitwise equal.
 //   k_coarse_l1         per level-1 block (one wave): R1 of its 32 nodes from
 //                       r gathered through the Morton map, summed per parent
 //                       in lane order from +0 exactly as the reference's owner
