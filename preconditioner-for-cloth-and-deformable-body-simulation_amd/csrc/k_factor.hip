@@ -17,7 +17,9 @@
 //                every FMA reads its pivot value from LDS) -- 15.0 ms at 1M
 //   k_factor_rb  (default) one wave per block, rows in VGPRs in 6x24 lane
 //                tiles, the pivot row broadcast through LDS, multipliers and
-//                quotients through DPP -- 2.3 ms at 1M (profiles/round1/ab)
+//                quotients through DPP -- 2.0 ms at 1M (profiles/round1/ab);
+//                MAS_FACTOR_VARIANT=3 forms the inverse on the matrix cores
+//                instead (form_mfma, not bitwise, 1.5 ms)
 #include <vector>
 
 #include "layout.h"
@@ -265,12 +267,78 @@ __device__ __forceinline__ void form_packed(const float* M, const float* dinv, f
     }
 }
 
+// Inv = M^T D M on the matrix cores (MAS_FACTOR_VARIANT=3): M = L^-1 (unit
+// lower triangular, packed in LDS), D = diag(D^-1).  Six 32x32 output tiles
+// (I <= J) of v_mfma_f32_32x32x2_f32: A = M[k..k+1][32I..32I+31]^T,
+// B = D^-1_k M[k..k+1][32J..32J+31]; rows k < 32 J are zero in B and skipped,
+// k runs downwards as in the reference's sum.  160 MFMAs per block replace
+// ~2.6k VALU instructions and ~20k LDS reads of form_packed.  An f32 MFMA is an
+// exact fmaf chain, but of M_ik * fl(D^-1_k M_jk) where the reference rounds
+// fl(M_ik M_jk) first: inverses agree within 4.6e-8 relative
+// (tests/test_gpu_factor_mfma.py), not bitwise; 1.96 -> 1.47 ms at 1M.
+typedef float v16f __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ float m_at(const float* M, int k, int i) {
+    return i < k ? M[m_row(k) + i] : (i == k ? 1.f : 0.f);
+}
+__device__ __forceinline__ v16f mfma_tile(const float* M, const float* dinv, int I, int J, int col, int kh) {
+    v16f acc = {};
+    for (int k0 = 94; k0 >= 32 * J; k0 -= 2) {
+        const int k = k0 + 1 - kh;  // the instruction is the fmaf chain k-half 0 then 1: strictly k-descending
+        const float a = m_at(M, k, 32 * I + col);
+        const float b = __fmul_rn(dinv[k], m_at(M, k, 32 * J + col));
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    return acc;
+}
+// All six tiles are accumulated first (96 accumulator registers: the
+// elimination's 144 tile registers are dead by now), then M's LDS is reused to
+// stage the packed inverse, which leaves as 1 KiB coalesced stores -- the
+// scattered 4-byte slot stores of form_packed are what bounds it (~0.9 ms of
+// the 1.95 ms factor at 1M; MFMA with scattered stores saved 4 %).
+// tileSlot: for tile t, accumulator register r and lane l, the packed slot of
+// the entry that register holds (0xFFFF: below the diagonal), 8 ushorts per
+// uint4 at [(2 t + r / 8) * 64 + l] -- 12 coalesced loads per lane instead of
+// 96 evaluations of slot_of (built on the host by upload_slot_table).
+__device__ __forceinline__ void form_mfma(float* M, const float* dinv, float* out, const uint4* __restrict__ tileSlot,
+                                          int lane) {
+    const int col = lane & 31, kh = lane >> 5;
+    uint4 sl[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) sl[q] = tileSlot[q * 64 + lane];
+    v16f acc[6];
+    acc[0] = mfma_tile(M, dinv, 0, 0, col, kh);
+    acc[1] = mfma_tile(M, dinv, 0, 1, col, kh);
+    acc[2] = mfma_tile(M, dinv, 1, 1, col, kh);
+    acc[3] = mfma_tile(M, dinv, 0, 2, col, kh);
+    acc[4] = mfma_tile(M, dinv, 1, 2, col, kh);
+    acc[5] = mfma_tile(M, dinv, 2, 2, col, kh);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every M read done before M is overwritten
+    __builtin_amdgcn_wave_barrier();
+    float* O = M;  // 4 656 <= kPackedM floats
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint4 w = sl[2 * t + (r >> 3)];
+            const int h = (r & 7) >> 1;
+            const unsigned word = h == 0 ? w.x : h == 1 ? w.y : h == 2 ? w.z : w.w;
+            const unsigned slot = (r & 1) ? word >> 16 : word & 0xFFFFu;
+            if (slot != 0xFFFFu) O[slot] = acc[t][r];
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const float4* O4 = reinterpret_cast<const float4*>(O);
+    float4* out4 = reinterpret_cast<float4*>(out);
+    for (int q = lane; q < kBlockF4; q += 64) out4[q] = O4[q];
+}
+
 // Register-blocked factor: LDS holds only the pivot row, D^-1 and the packed
 // M (~19.5 KB -> 8 blocks per CU at <= 256 VGPRs), the block is loaded from
 // HBM straight into the lane tiles, and the inverse entries are stored
 // straight to their slots (slot_of) instead of staging the packed output.
+template <bool MFMA>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_rb(
-    const float* __restrict__ dense, float* __restrict__ inv) {
+    const float* __restrict__ dense, float* __restrict__ inv, const uint4* __restrict__ tileSlot) {
     __shared__ __attribute__((aligned(16))) float M[kPackedM];
     __shared__ __attribute__((aligned(16))) float piv[96];
     __shared__ float dinv[96];
@@ -314,7 +382,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
     }
     __syncthreads();
-    form_packed(M, dinv, inv + blk * kBlockFloats, t, 64);
+    if (MFMA) form_mfma(M, dinv, inv + blk * kBlockFloats, tileSlot, t);  // one wave: no barrier around M
+    else form_packed(M, dinv, inv + blk * kBlockFloats, t, 64);
 }
 
 int upload_slot_table(mas_context* h) {
@@ -326,7 +395,21 @@ int upload_slot_table(mas_context* h) {
     }
     int rc = ensure(h, h->slotTable, tab.size() * 4);
     if (rc) return rc;
-    return hip_check(h, hipMemcpy(h->slotTable.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), "H2D slots");
+    if ((rc = hip_check(h, hipMemcpy(h->slotTable.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), "H2D slots")))
+        return rc;
+    // form_mfma's per-(tile, register, lane) slots: MFMA 32x32 D layout, lane l,
+    // register r -> row 8 (r / 4) + 4 (l / 32) + r % 4, column l % 32
+    const int tI[6] = {0, 0, 1, 0, 1, 2}, tJ[6] = {0, 1, 1, 2, 2, 2};
+    std::vector<uint16_t> ts(12 * 64 * 8);
+    for (int t = 0; t < 6; ++t)
+        for (int r = 0; r < 16; ++r)
+            for (int l = 0; l < 64; ++l) {
+                const int i = 32 * tI[t] + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3), j = 32 * tJ[t] + (l & 31);
+                ts[((2 * t + (r >> 3)) * 64 + l) * 8 + (r & 7)] =
+                    (tI[t] < tJ[t] || i <= j) ? (uint16_t)slot_of(i, j) : (uint16_t)0xFFFF;
+            }
+    if ((rc = ensure(h, h->tileSlot, ts.size() * 2))) return rc;
+    return hip_check(h, hipMemcpy(h->tileSlot.p, ts.data(), ts.size() * 2, hipMemcpyHostToDevice), "H2D tile slots");
 }
 
 int copy_block_inverse(mas_context* h, int blk, float* out96) {
@@ -354,7 +437,8 @@ int run_factor(mas_context* h, hipStream_t s) {
         k_factor<<<h->nBlk, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv);
     } else {
         k_identity_fix<<<cdiv(h->nBlk * 32, 256), 256, 0, s>>>(dense, h->nBlk * 32);
-        k_factor_rb<<<h->nBlk, 64, 0, s>>>(dense, inv);
+        if (h->factorVariant == 3) k_factor_rb<true><<<h->nBlk, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot));
+        else k_factor_rb<false><<<h->nBlk, 64, 0, s>>>(dense, inv, nullptr);
     }
     return hip_check(h, hipGetLastError(), "factor kernel");
 }
