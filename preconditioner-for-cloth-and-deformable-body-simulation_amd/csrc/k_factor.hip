@@ -17,9 +17,10 @@
 //                every FMA reads its pivot value from LDS) -- 15.0 ms at 1M
 //   k_factor_rb  (default) one wave per block, rows in VGPRs in 6x24 lane
 //                tiles, the pivot row broadcast through LDS, multipliers and
-//                quotients through DPP -- 2.0 ms at 1M (profiles/round1/ab);
+//                quotients through DPP, inverse staged in LDS and stored
+//                coalesced -- 1.63 ms at 1M (profiles/round1/ab);
 //                MAS_FACTOR_VARIANT=3 forms the inverse on the matrix cores
-//                instead (form_mfma, not bitwise, 1.5 ms)
+//                instead (form_mfma, not bitwise, 1.47 ms)
 #include <vector>
 
 #include "layout.h"
@@ -222,18 +223,27 @@ __device__ __forceinline__ int m_row(int k) {
 }
 constexpr int kPackedM = 4800;
 
-// Inv entries from the packed M (unit diagonal), tiles of 4x4 (I <= J), k
-// descending from 95 with (fmul, fma) as the reference; stored to slot_of.
-__device__ __forceinline__ void form_packed(const float* M, const float* dinv, float* out, int t, int nThreads) {
-    for (int tile = t; tile < 300; tile += nThreads) {
-        int J = 0, rem = tile;
-        while (rem > J) { rem -= J + 1; ++J; }
-        const int I = rem;
-        float acc[4][4];
+// Inv entries from the packed M (unit diagonal) in 4x4 tiles (I <= J), k
+// descending from 95 with (fmul, fma) as the reference.  One wave: each lane
+// keeps its <= 5 tiles (tile = lane + 64 t) in registers, then M's LDS is
+// reused to assemble the packed inverse (slots from the host-built table
+// valuSlot: 16 ushorts per tile, 0xFFFF below the diagonal), which leaves as
+// 1 KiB coalesced stores: the scattered 4-byte slot stores this replaced made
+// the formation ~0.9 ms of a 1.96 ms factor at 1M (now 1.63 ms, bitwise equal).
+__device__ __forceinline__ void form_packed_staged(float* M, const float* dinv, float* out,
+                                                   const uint4* __restrict__ valuSlot, int lane) {
+    float acc[5][4][4];
+#pragma unroll
+    for (int tt = 0; tt < 5; ++tt) {
+        const int tile = lane + 64 * tt;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
+            for (int b = 0; b < 4; ++b) acc[tt][a][b] = 0.f;
+        if (tile >= 300) continue;
+        int J = 0, rem = tile;
+        while (rem > J) { rem -= J + 1; ++J; }
+        const int I = rem;
         for (int k = 95; k >= 4 * J + 3; --k) {
             const int base = m_row(k);
             const float4 mi = *reinterpret_cast<const float4*>(&M[base + 4 * I]);
@@ -243,7 +253,7 @@ __device__ __forceinline__ void form_packed(const float* M, const float* dinv, f
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b < 4; ++b) acc[a][b] = __fmaf_rn(d, __fmul_rn(fi[a], fj[b]), acc[a][b]);
+                for (int b = 0; b < 4; ++b) acc[tt][a][b] = __fmaf_rn(d, __fmul_rn(fi[a], fj[b]), acc[tt][a][b]);
         }
 #pragma unroll
         for (int kk = 2; kk >= 0; --kk) {
@@ -255,16 +265,36 @@ __device__ __forceinline__ void form_packed(const float* M, const float* dinv, f
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b <= kk; ++b) acc[a][b] = __fmaf_rn(d, __fmul_rn(fi[a], fj[b]), acc[a][b]);
+                for (int b = 0; b <= kk; ++b) acc[tt][a][b] = __fmaf_rn(d, __fmul_rn(fi[a], fj[b]), acc[tt][a][b]);
         }
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int i = 4 * I + a, j = 4 * J + b;
-                if (i <= j) out[slot_of(i, j)] = acc[a][b];
-            }
     }
+    uint4 sl[10];
+#pragma unroll
+    for (int tt = 0; tt < 5; ++tt) {
+        const int tile = lane + 64 * tt < 300 ? lane + 64 * tt : 0;
+        sl[2 * tt] = valuSlot[2 * tile];
+        sl[2 * tt + 1] = valuSlot[2 * tile + 1];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every M read done before M is overwritten
+    __builtin_amdgcn_wave_barrier();
+    float* O = M;
+#pragma unroll
+    for (int tt = 0; tt < 5; ++tt) {
+        if (lane + 64 * tt >= 300) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const uint4 w = sl[2 * tt + (e >> 3)];
+            const int h = (e & 7) >> 1;
+            const unsigned word = h == 0 ? w.x : h == 1 ? w.y : h == 2 ? w.z : w.w;
+            const unsigned slot = (e & 1) ? word >> 16 : word & 0xFFFFu;
+            if (slot != 0xFFFFu) O[slot] = acc[tt][e >> 2][e & 3];
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const float4* O4 = reinterpret_cast<const float4*>(O);
+    float4* out4 = reinterpret_cast<float4*>(out);
+    for (int q = lane; q < kBlockF4; q += 64) out4[q] = O4[q];
 }
 
 // Inv = M^T D M on the matrix cores (MAS_FACTOR_VARIANT=3): M = L^-1 (unit
@@ -272,7 +302,7 @@ __device__ __forceinline__ void form_packed(const float* M, const float* dinv, f
 // (I <= J) of v_mfma_f32_32x32x2_f32: A = M[k..k+1][32I..32I+31]^T,
 // B = D^-1_k M[k..k+1][32J..32J+31]; rows k < 32 J are zero in B and skipped,
 // k runs downwards as in the reference's sum.  160 MFMAs per block replace
-// ~2.6k VALU instructions and ~20k LDS reads of form_packed.  An f32 MFMA is an
+// ~2.6k VALU instructions and ~20k LDS reads of form_packed_staged.  An f32 MFMA is an
 // exact fmaf chain, but of M_ik * fl(D^-1_k M_jk) where the reference rounds
 // fl(M_ik M_jk) first: inverses agree within 4.6e-8 relative
 // (tests/test_gpu_factor_mfma.py), not bitwise; 1.96 -> 1.47 ms at 1M.
@@ -292,9 +322,8 @@ __device__ __forceinline__ v16f mfma_tile(const float* M, const float* dinv, int
 }
 // All six tiles are accumulated first (96 accumulator registers: the
 // elimination's 144 tile registers are dead by now), then M's LDS is reused to
-// stage the packed inverse, which leaves as 1 KiB coalesced stores -- the
-// scattered 4-byte slot stores of form_packed are what bounds it (~0.9 ms of
-// the 1.95 ms factor at 1M; MFMA with scattered stores saved 4 %).
+// stage the packed inverse, which leaves as 1 KiB coalesced stores (with
+// scattered slot stores the MFMA formation saved only 4 %).
 // tileSlot: for tile t, accumulator register r and lane l, the packed slot of
 // the entry that register holds (0xFFFF: below the diagonal), 8 ushorts per
 // uint4 at [(2 t + r / 8) * 64 + l] -- 12 coalesced loads per lane instead of
@@ -334,11 +363,12 @@ __device__ __forceinline__ void form_mfma(float* M, const float* dinv, float* ou
 
 // Register-blocked factor: LDS holds only the pivot row, D^-1 and the packed
 // M (~19.5 KB -> 8 blocks per CU at <= 256 VGPRs), the block is loaded from
-// HBM straight into the lane tiles, and the inverse entries are stored
-// straight to their slots (slot_of) instead of staging the packed output.
+// HBM straight into the lane tiles, and M's LDS is reused to stage the packed
+// inverse once M is consumed.
 template <bool MFMA>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_rb(
-    const float* __restrict__ dense, float* __restrict__ inv, const uint4* __restrict__ tileSlot) {
+    const float* __restrict__ dense, float* __restrict__ inv, const uint4* __restrict__ tileSlot,
+    const uint4* __restrict__ valuSlot) {
     __shared__ __attribute__((aligned(16))) float M[kPackedM];
     __shared__ __attribute__((aligned(16))) float piv[96];
     __shared__ float dinv[96];
@@ -383,7 +413,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     }
     __syncthreads();
     if (MFMA) form_mfma(M, dinv, inv + blk * kBlockFloats, tileSlot, t);  // one wave: no barrier around M
-    else form_packed(M, dinv, inv + blk * kBlockFloats, t, 64);
+    else form_packed_staged(M, dinv, inv + blk * kBlockFloats, valuSlot, t);
 }
 
 int upload_slot_table(mas_context* h) {
@@ -408,8 +438,20 @@ int upload_slot_table(mas_context* h) {
                 ts[((2 * t + (r >> 3)) * 64 + l) * 8 + (r & 7)] =
                     (tI[t] < tJ[t] || i <= j) ? (uint16_t)slot_of(i, j) : (uint16_t)0xFFFF;
             }
-    if ((rc = ensure(h, h->tileSlot, ts.size() * 2))) return rc;
-    return hip_check(h, hipMemcpy(h->tileSlot.p, ts.data(), ts.size() * 2, hipMemcpyHostToDevice), "H2D tile slots");
+    if ((rc = ensure(h, h->tileSlot, ts.size() * 2)) ||
+        (rc = hip_check(h, hipMemcpy(h->tileSlot.p, ts.data(), ts.size() * 2, hipMemcpyHostToDevice), "H2D tile slots")))
+        return rc;
+    // form_packed_staged's slots: 4x4 tile (I, J), I <= J, tile = J (J + 1) / 2 + I, entry 4 a + b
+    std::vector<uint16_t> vs(300 * 16);
+    for (int J = 0, tile = 0; J < 24; ++J)
+        for (int I = 0; I <= J; ++I, ++tile)
+            for (int a = 0; a < 4; ++a)
+                for (int b = 0; b < 4; ++b) {
+                    const int i = 4 * I + a, j = 4 * J + b;
+                    vs[tile * 16 + 4 * a + b] = i <= j ? (uint16_t)slot_of(i, j) : (uint16_t)0xFFFF;
+                }
+    if ((rc = ensure(h, h->valuSlot, vs.size() * 2))) return rc;
+    return hip_check(h, hipMemcpy(h->valuSlot.p, vs.data(), vs.size() * 2, hipMemcpyHostToDevice), "H2D valu slots");
 }
 
 int copy_block_inverse(mas_context* h, int blk, float* out96) {
@@ -437,8 +479,10 @@ int run_factor(mas_context* h, hipStream_t s) {
         k_factor<<<h->nBlk, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv);
     } else {
         k_identity_fix<<<cdiv(h->nBlk * 32, 256), 256, 0, s>>>(dense, h->nBlk * 32);
-        if (h->factorVariant == 3) k_factor_rb<true><<<h->nBlk, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot));
-        else k_factor_rb<false><<<h->nBlk, 64, 0, s>>>(dense, inv, nullptr);
+        if (h->factorVariant == 3)
+            k_factor_rb<true><<<h->nBlk, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot));
+        else
+            k_factor_rb<false><<<h->nBlk, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot));
     }
     return hip_check(h, hipGetLastError(), "factor kernel");
 }

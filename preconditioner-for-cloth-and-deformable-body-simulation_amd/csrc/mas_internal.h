@@ -79,7 +79,7 @@ struct mas_context {
     mas::Buffer rawContacts, stencilFlags, stencilSlots, stencils;
     mas::Buffer fineMask, nextMask, bankCount, bankPrefix, levelTotal;
     mas::Buffer cst, goingNext, vmap, coarseTables;
-    mas::Buffer dense, inv, slotTable, tileSlot;
+    mas::Buffer dense, inv, slotTable, tileSlot, valuSlot;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, shardPos1, l1src;
@@ -104,7 +104,7 @@ struct mas_context {
         mas::Buffer* all[] = {&pos, &starts, &idx, &edges, &faces, &morton, &mortonSorted, &iota, &s2o, &o2s,
                               &nbrNum, &nbr, &nbrNumRem, &nbrRem, &aabbPartial, &rawContacts, &stencilFlags,
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
-                              &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &tileSlot, &additional, &od,
+                              &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &tileSlot, &valuSlot, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
                               &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
