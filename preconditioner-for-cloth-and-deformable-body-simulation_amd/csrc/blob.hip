@@ -203,6 +203,8 @@ int mas_blob_size(mas_handle h, size_t* out_bytes) {
 int mas_save_blob(mas_handle h, void* dst, size_t capacity, size_t* written) {
     if (!h) return MAS_ERR_ARG;
     hipSetDevice(h->device);
+    if (h->prepared && h->l1First.empty())  // computed lazily after Prepare (k_shard.hip)
+        if (int rc = compute_l1_first(h, h->stream)) return rc;
     return blob_save(h, dst, capacity, written);
 }
 

@@ -193,6 +193,10 @@ int mas_shard_plan(int nV, const int* l1_first, int rank, int world, mas_shard* 
 int mas_shard_setup(mas_handle h, int rank, int world, mas_shard* out) {
     if (!h || !out) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "shard setup before prepare");
+    if (h->l1First.empty()) {  // first shard call after a Prepare (kept out of Prepare's time)
+        hipSetDevice(h->device);
+        if (int rc = compute_l1_first(h, h->stream)) return rc;
+    }
     return mas_shard_plan(h->nV, h->l1First.data(), rank, world, out);
 }
 

@@ -34,7 +34,7 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     if (nCoarseNodes > 0 && (rc = hip_check(h, hipMemsetAsync(h->Rc.p, 0, (size_t)nCoarseNodes * 16, s), "memset Rc")))
         return rc;
     if ((rc = prepare_apply_tables(h, s))) return rc;
-    if ((rc = compute_l1_first(h, s))) return rc;
+    h->l1First.clear();  // per-bank level-1 starts: computed on first use (sharding, blob save)
     h->shardWorld = 0;
     hipEventRecord(h->ev[3], s);
     if ((rc = hip_check(h, hipStreamSynchronize(s), "prepare sync"))) return rc;
