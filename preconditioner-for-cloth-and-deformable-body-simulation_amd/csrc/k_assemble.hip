@@ -33,6 +33,8 @@
 // accumulate with fp32 atomics, as the reference does at CPU_THREAD_NUM > 1.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "mas_internal.h"
 
 namespace mas {
@@ -76,51 +78,98 @@ __device__ __forceinline__ void add_colmajor(float* e, const float* __restrict__
 // terms instead of before (.cpp:1201-1271): a reassociation of fp32 sums the
 // reference's multi-threaded atomics do not fix either (B-10).
 enum { kContactAdditional = 1, kContactPairs = 2 };
-__global__ __launch_bounds__(256) void k_collision_hessian(const DevStencil* __restrict__ st, int n, int mode,
-                                                           const int* __restrict__ gn, int L,
-                                                           float* __restrict__ dense, float* __restrict__ additional) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    DevStencil s = st[i];
-    float ds[3] = {__fmul_rn(s.dir[0], s.stiff), __fmul_rn(s.dir[1], s.stiff), __fmul_rn(s.dir[2], s.stiff)};
-    float hm[3][3];  // OuterProduct(d, d * stiff), SeMatrix.h:352-363
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) hm[r][c] = __fmul_rn(s.dir[r], ds[c]);
-    for (int it = 0; mode == kContactAdditional && it < s.n; ++it) {  // .cpp:1214-1217: additional[idx] += h w^2
-        const float w2 = __fmul_rn(s.w[it], s.w[it]);
-        float* a = additional + 9 * (size_t)s.idx[it];
+constexpr int kContactThreads = 1024, kContactBlocks = 256;
+// Random contact pairs mostly meet only in the top level's single block, so
+// every stencil's 18 atomics per pair hit the same 9 216 floats of one dense
+// block (and, for pairs meeting one level lower, the 288 floats of the top
+// nodes' additional terms): 10.8 M same-address float atomics for 100k VF
+// contacts, 0.6 ms per pass.  When the top level is one block, each
+// workgroup therefore accumulates those targets in LDS (LDS float atomics)
+// and adds its partial sums to HBM once at the end -- 64 workgroups, so 64
+// global adds per target.  Other targets are added directly as before.  Sums
+// of contact terms are atomic (order-free) in the reference too (B-10).
+__global__ __launch_bounds__(kContactThreads) void k_collision_hessian(const DevStencil* __restrict__ st, int n,
+                                                                       int mode, const int* __restrict__ gn, int L,
+                                                                       int topNode, float* __restrict__ dense,
+                                                                       float* __restrict__ additional) {
+    __shared__ float priv[kDenseFloats];  // the top block (pairs) or the top nodes' additional terms (288)
+    const bool privatize = topNode >= 0;
+    const unsigned topBank = privatize ? (unsigned)topNode >> 5 : 0xffffffffu;
+    const int nPriv = mode == kContactPairs ? kDenseFloats : 32 * 9;
+    if (privatize)
+        for (int e = threadIdx.x; e < nPriv; e += blockDim.x) priv[e] = 0.f;
+    __syncthreads();
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const DevStencil s = st[i];
+        float ds[3] = {__fmul_rn(s.dir[0], s.stiff), __fmul_rn(s.dir[1], s.stiff), __fmul_rn(s.dir[2], s.stiff)};
+        float hm[3][3];  // OuterProduct(d, d * stiff), SeMatrix.h:352-363
         for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) atomicAdd(a + r * 3 + c, __fmul_rn(hm[r][c], w2));
-    }
-    for (int a = 0; a < s.n; ++a)  // AdditionalSchwarzHessian2, .cpp:1164-1199
-        for (int b = a + 1; b < s.n; ++b) {
-            const float ww = __fmul_rn(s.w[a], s.w[b]);
-            unsigned my = (unsigned)s.idx[a], ot = (unsigned)s.idx[b];
-            const int level = climb(gn, L, my, ot);
-            if (level >= L) continue;
-            if (mode == kContactPairs) {
-                float* e0 = entry(dense, my, ot);
-                float* e1 = entry(dense, ot, my);
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) {
-                        const float t = __fmul_rn(ww, hm[r][c]);
-                        atomicAdd(e0 + r * 96 + c, t);
-                        atomicAdd(e1 + r * 96 + c, t);
-                    }
-            } else if (level < L - 1) {
-                const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) {
-                        const float t = __fmul_rn(ww, hm[r][c]);
-                        if (pm == po) {
-                            atomicAdd(additional + 9 * (size_t)pm + r * 3 + c, __fmul_rn(t, 2.0f));
-                        } else {
-                            atomicAdd(additional + 9 * (size_t)pm + r * 3 + c, t);
-                            atomicAdd(additional + 9 * (size_t)po + r * 3 + c, t);
+            for (int c = 0; c < 3; ++c) hm[r][c] = __fmul_rn(s.dir[r], ds[c]);
+        for (int it = 0; mode == kContactAdditional && it < s.n; ++it) {  // .cpp:1214-1217: additional[idx] += h w^2
+            const float w2 = __fmul_rn(s.w[it], s.w[it]);
+            float* a = additional + 9 * (size_t)s.idx[it];
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) atomicAdd(a + r * 3 + c, __fmul_rn(hm[r][c], w2));
+        }
+        for (int a = 0; a < s.n; ++a)  // AdditionalSchwarzHessian2, .cpp:1164-1199
+            for (int b = a + 1; b < s.n; ++b) {
+                const float ww = __fmul_rn(s.w[a], s.w[b]);
+                unsigned my = (unsigned)s.idx[a], ot = (unsigned)s.idx[b];
+                const int level = climb(gn, L, my, ot);
+                if (level >= L) continue;
+                // LDS and HBM targets on separate paths: one pointer that may be
+                // either compiles to flat atomics, which serialise on LDS
+                if (mode == kContactPairs) {
+                    float t[9];
+                    for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e / 3][e % 3]);
+                    if ((my >> 5) == topBank) {
+                        const int o0 = (3 * (my & 31)) * 96 + 3 * (ot & 31), o1 = (3 * (ot & 31)) * 96 + 3 * (my & 31);
+                        for (int e = 0; e < 9; ++e) {
+                            atomicAdd(&priv[o0 + (e / 3) * 96 + e % 3], t[e]);
+                            atomicAdd(&priv[o1 + (e / 3) * 96 + e % 3], t[e]);
+                        }
+                    } else {
+                        float* e0 = entry(dense, my, ot);
+                        float* e1 = entry(dense, ot, my);
+                        for (int e = 0; e < 9; ++e) {
+                            atomicAdd(e0 + (e / 3) * 96 + e % 3, t[e]);
+                            atomicAdd(e1 + (e / 3) * 96 + e % 3, t[e]);
                         }
                     }
+                } else if (level < L - 1) {
+                    const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
+                    float t[9];
+                    for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e / 3][e % 3]);
+                    if ((pm >> 5) == topBank) {  // then po is a top node too
+                        const int om = 9 * (pm & 31), oo = 9 * (po & 31);
+                        for (int e = 0; e < 9; ++e) {
+                            if (pm == po) {
+                                atomicAdd(&priv[om + e], __fmul_rn(t[e], 2.0f));
+                            } else {
+                                atomicAdd(&priv[om + e], t[e]);
+                                atomicAdd(&priv[oo + e], t[e]);
+                            }
+                        }
+                    } else {
+                        float* am = additional + 9 * (size_t)pm;
+                        float* ao = additional + 9 * (size_t)po;
+                        for (int e = 0; e < 9; ++e) {
+                            if (pm == po) {
+                                atomicAdd(am + e, __fmul_rn(t[e], 2.0f));
+                            } else {
+                                atomicAdd(am + e, t[e]);
+                                atomicAdd(ao + e, t[e]);
+                            }
+                        }
+                    }
+                }
             }
-        }
+    }
+    if (!privatize) return;
+    __syncthreads();
+    float* dst = mode == kContactPairs ? dense + (size_t)topBank * kDenseFloats : additional + 9 * (size_t)(topBank * 32);
+    for (int e = threadIdx.x; e < nPriv; e += blockDim.x)
+        if (priv[e] != 0.f) atomicAdd(dst + e, priv[e]);
 }
 
 // .cpp:1236-1252: coarse additional -> own diagonal and every ancestor.
@@ -404,16 +453,19 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     float* add = P<float>(h->additional);
     const int* gn = P<int>(h->goingNext);
     const int begin1 = h->levelSize[3];
+    // privatize the top level's targets when it is one block (k_collision_hessian)
+    const int topNode = (L > 1 && ceil32(h->levelSize[2 * (L - 1)]) == 32) ? h->levelSize[2 * (L - 1) + 1] : -1;
+    const int gContact = std::max(1, std::min(kContactBlocks, cdiv(h->nStencil, kContactThreads)));
     if (h->nStencil) {
-        k_collision_hessian<<<cdiv(h->nStencil, 256), 256, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
-                                                                   kContactAdditional, gn, L, dense, add);
+        k_collision_hessian<<<gContact, kContactThreads, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
+                                                                 kContactAdditional, gn, L, topNode, dense, add);
         if (tc > begin1) k_coarse_additional<<<cdiv(tc - begin1, 256), 256, 0, s>>>(begin1, tc, gn, add, dense);
     }
     k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
                                               d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt));
     if (h->nStencil)
-        k_collision_hessian<<<cdiv(h->nStencil, 256), 256, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
-                                                                   kContactPairs, gn, L, dense, add);
+        k_collision_hessian<<<gContact, kContactThreads, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
+                                                                 kContactPairs, gn, L, topNode, dense, add);
     if (L == 1) return hip_check(h, hipGetLastError(), "assembly kernels");
 
     // coarse edge records in (u, k) order

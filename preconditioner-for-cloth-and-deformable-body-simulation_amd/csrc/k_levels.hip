@@ -109,8 +109,11 @@ __global__ __launch_bounds__(256) void k_collision_connect(const DevStencil* __r
                 msk[b] |= 1u << (my & 31);
             }
         }
+    // coarse levels: many stencils set the same bits of the same few nodes;
+    // skip the atomic when they are all set already (OR is idempotent, so a
+    // stale read only costs a redundant atomic)
     for (int k = 0; k < s.n; ++k)
-        if (msk[k]) atomicOr(&connect[idx[k]], msk[k]);
+        if (msk[k] && (connect[idx[k]] & msk[k]) != msk[k]) atomicOr(&connect[idx[k]], msk[k]);
 }
 
 // ---------------------------------------------------------------------------
