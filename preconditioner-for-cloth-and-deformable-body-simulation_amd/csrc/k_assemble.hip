@@ -20,9 +20,9 @@
 //                 entries (oldDiagonal, .cpp:1270-1298), count of coarse edges
 //   k_records     coarse edges (u, k) with first common-bank level 1..L-1, in
 //                 (u, k) order
-//   k_fold_entries  one thread per coarse entry (row, col), (key, mat)
+//   k_fold_entries, k_fold_long  per coarse entry (row, col), (key, mat)
 //                 pairs sorted stably by key = (row, col): entry += mat in
-//                 (u, k) order
+//                 (u, k) order (short runs: a thread; long runs: a wave)
 //   k_diag1       one thread per level-0 bank: diag(anc1(u)) += od(u) (.cpp:1309-1312)
 //   k_term_*, k_table_fold  the diagTable fold (.cpp:1299-1343) per level-l
 //                 node (l >= 2): over member vertices in order, level-(l-1)
@@ -297,7 +297,23 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, const int* __res
     }
 }
 
-// one thread per run of equal (row, col) in the stably sorted record keys
+// The (row, col) runs of the stably sorted record keys are folded strictly
+// left, so a run's fold is one dependent chain; what is parallel is its loads.
+// Run lengths are very uneven (cloth 1M, 4 levels: ~10 records per level-1
+// entry, hundreds per level-3 entry), and a thread walking a long run pays two
+// dependent load latencies per record (mats, then off9) -- the longest runs set
+// the kernel time.  So:
+//   k_fold_entries  one thread per run shorter than kLongRun; records are
+//                 loaded kFoldBatch at a time (all loads issued, then the adds
+//                 in order).
+//   k_fold_long   one wave per 64 sorted positions; it folds, one after the
+//                 other, the runs of kLongRun or more that start there: 64
+//                 records per step are loaded by the lanes into LDS, then lanes
+//                 0..8 each fold one of the nine entries over them in order.
+// (Collecting the long runs into a list with a counter was measured first: ~60k
+// atomics on one address serialised and cost ~300 us.)
+constexpr int kLongRun = 16, kFoldBatch = 8;
+
 __global__ __launch_bounds__(256) void k_fold_entries(int n, const unsigned long long* __restrict__ keys,
                                                       const int* __restrict__ mats, const float* __restrict__ off9,
                                                       float* __restrict__ dense) {
@@ -305,17 +321,67 @@ __global__ __launch_bounds__(256) void k_fold_entries(int n, const unsigned long
     if (i >= n) return;
     const unsigned long long key = keys[i];
     if (key == ~0ull || (i > 0 && keys[i - 1] == key)) return;
+    if (i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key) return;  // sorted: >= kLongRun records, k_fold_long
     float* e = entry(dense, (unsigned)(key >> 32), (unsigned)(key & 0xffffffffu));
     float acc[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
-    for (int j = i; j < n && keys[j] == key; ++j) {
-        const float* m = off9 + 9 * (size_t)mats[j];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[c * 3 + r]);
+    for (int j0 = i; j0 < i + kLongRun; j0 += kFoldBatch) {
+        bool in[kFoldBatch];
+        float m[kFoldBatch][9];
+#pragma unroll
+        for (int t = 0; t < kFoldBatch; ++t) {
+            const int j = j0 + t;
+            in[t] = j < n && keys[j] == key;
+            const float* src = off9 + 9 * (size_t)(in[t] ? mats[j] : mats[i]);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) m[t][q] = src[q];
+        }
+#pragma unroll
+        for (int t = 0; t < kFoldBatch; ++t)
+            if (in[t])
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[t][c * 3 + r]);
+        if (!in[kFoldBatch - 1]) break;
     }
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
+}
+
+__global__ __launch_bounds__(64) void k_fold_long(int n, const unsigned long long* __restrict__ keys,
+                                                  const int* __restrict__ mats, const float* __restrict__ off9,
+                                                  float* __restrict__ dense) {
+    __shared__ float T[9 * 65];  // T[q * 65 + record]: off9 component q; stride 65 keeps lanes 0..8 on distinct banks
+    const int lane = threadIdx.x;
+    const int r = lane / 3, c = lane % 3;
+    const int i = blockIdx.x * 64 + lane;
+    bool isLong = false;
+    if (i < n) {
+        const unsigned long long key = keys[i];
+        isLong = key != ~0ull && (i == 0 || keys[i - 1] != key) && i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key;
+    }
+    for (unsigned long long starts = __ballot(isLong); starts; starts &= starts - 1) {
+        const int start = blockIdx.x * 64 + __ffsll((long long)starts) - 1;
+        const unsigned long long key = keys[start];
+        float* e = entry(dense, (unsigned)(key >> 32), (unsigned)(key & 0xffffffffu));
+        float acc = lane < 9 ? e[r * 96 + c] : 0.f;
+        for (int j0 = start;; j0 += 64) {
+            const int j = j0 + lane;
+            const bool in = j < n && keys[j] == key;
+            const int cnt = __popcll(__ballot(in));  // the run is contiguous: lanes 0..cnt-1
+            if (in) {
+                const float* src = off9 + 9 * (size_t)mats[j];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) T[q * 65 + lane] = src[q];
+            }
+            __syncthreads();
+            if (lane < 9)
+                for (int k = 0; k < cnt; ++k) acc = __fadd_rn(acc, T[(c * 3 + r) * 65 + k]);
+            __syncthreads();
+            if (cnt < 64) break;
+        }
+        if (lane < 9) e[r * 96 + c] = acc;
+    }
 }
 
 // level-1 diagonal: one thread per level-0 bank, members in lane order
@@ -504,6 +570,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
             return rc;
         k_fold_entries<<<cdiv(nRec, 256), 256, 0, s>>>(nRec, P<unsigned long long>(h->recKeysSorted),
                                                        P<int>(h->recIdsSorted), d_off9, dense);
+        k_fold_long<<<cdiv(nRec, 64), 64, 0, s>>>(nRec, P<unsigned long long>(h->recKeysSorted),
+                                                  P<int>(h->recIdsSorted), d_off9, dense);
     }
     k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
 
