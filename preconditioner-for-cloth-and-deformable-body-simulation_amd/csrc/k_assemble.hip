@@ -71,7 +71,7 @@ __device__ __forceinline__ void add_colmajor(float* e, const float* __restrict__
 // ---------------------------------------------------------------------------
 
 // Two passes over the stencils: ADDITIONAL (the per-vertex w^2 h terms and
-// the parent terms, read by the level-0 assembly and k_coarse_additional) runs
+// the parent terms, read by the level-0 assembly and k_additional_up) runs
 // first; PAIRS (the h w_a w_b terms into the blocks) runs after the level-0
 // blocks are written whole, so the fine blocks need no memset and no
 // read-back.  For the fine entries this adds the contact terms after the CSR
@@ -173,22 +173,50 @@ __global__ __launch_bounds__(kContactThreads) void k_collision_hessian(const Dev
 }
 
 // .cpp:1236-1252: coarse additional -> own diagonal and every ancestor.
-__global__ __launch_bounds__(256) void k_coarse_additional(int begin1, int tc, const int* __restrict__ gn,
-                                                           const float* __restrict__ additional,
-                                                           float* __restrict__ dense) {
-    const int vid = begin1 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (vid >= tc) return;
-    const float* a = additional + 9 * (size_t)vid;
-    bool any = false;
-    for (int e = 0; e < 9; ++e) any |= a[e] != 0.f;
-    if (!any) return;
-    int my = vid;
-    while (my < tc) {
-        float* d = entry(dense, my, my);
+// Contact terms of coarse nodes reach their own diagonal and every ancestor's
+// (.cpp:1214-1217 then the hierarchy climb): diag(P) += S(P), where S(P) is
+// add(P) plus the S of P's children.  Adding add(c) to each ancestor with one
+// atomic per level (the first form) put ~33k same-address atomics on the top
+// node (86 us).  Instead S climbs one level per launch: the children of a
+// level-l node all sit in one 32-node bank of level l-1 (a level-l node is a
+// component of such a bank), so one half-wave per child bank sums S over the
+// children of each parent in lane order and the lowest child writes
+// S(parent) = add(parent) + sum into `additional` (in place) and adds it to the
+// parent's diagonal -- a single writer per target, no atomics.  (Sums of
+// contact terms are order-free in the reference, B-10.)
+__global__ __launch_bounds__(64) void k_additional_up(int beginC, int nC, int tc, bool ownDiag,
+                                                      const int* __restrict__ gn, float* __restrict__ additional,
+                                                      float* __restrict__ dense) {
+    __shared__ float S[64][9];
+    __shared__ int par[64];
+    const int t = threadIdx.x, c = beginC + blockIdx.x * 64 + t;
+    const bool live = c < beginC + nC;
+    const int p = live ? gn[c] : -1;
+    float a[9];
+    for (int e = 0; e < 9; ++e) a[e] = live ? additional[9 * (size_t)c + e] : 0.f;
+    if (live && ownDiag) {  // level-1 nodes: their own diagonal
+        float* d = entry(dense, c, c);
         for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) atomicAdd(d + r * 96 + c, a[r * 3 + c]);
-        my = gn[my];
+            for (int q = 0; q < 3; ++q) d[r * 96 + q] = __fadd_rn(d[r * 96 + q], a[r * 3 + q]);
     }
+    for (int e = 0; e < 9; ++e) S[t][e] = a[e];
+    par[t] = p;
+    __syncthreads();
+    if (!live || p >= tc) return;
+    const int b0 = t & ~31;
+    for (int j = b0; j < t; ++j)
+        if (par[j] == p) return;  // not the lowest child of p
+    float sum[9];
+    for (int e = 0; e < 9; ++e) sum[e] = additional[9 * (size_t)p + e];
+    for (int j = t; j < b0 + 32; ++j)
+        if (par[j] == p)
+            for (int e = 0; e < 9; ++e) sum[e] = __fadd_rn(sum[e], S[j][e]);
+    float* d = entry(dense, p, p);
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q) {
+            additional[9 * (size_t)p + r * 3 + q] = sum[r * 3 + q];
+            d[r * 96 + q] = __fadd_rn(d[r * 96 + q], sum[r * 3 + q]);
+        }
 }
 
 // ---------------------------------------------------------------------------
@@ -384,18 +412,36 @@ __global__ __launch_bounds__(64) void k_fold_long(int n, const unsigned long lon
     }
 }
 
-// level-1 diagonal: one thread per level-0 bank, members in lane order
+// level-1 diagonal: one thread per level-0 bank, members in lane order.  The
+// bank's vertices mostly share one level-1 node, so the running entry stays in
+// registers and is written back only when the parent changes (the same left
+// fold, without a dependent read-modify-write of HBM per vertex).
 __global__ __launch_bounds__(256) void k_diag1(int nV, const int* __restrict__ gn, const float* __restrict__ od,
                                                float* __restrict__ dense) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w * 32 >= nV) return;
-    for (int u = w * 32; u < w * 32 + 32 && u < nV; ++u) {
+    const int end = min(w * 32 + 32, nV);
+    unsigned cur = (unsigned)gn[w * 32];
+    float acc[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = entry(dense, cur, cur)[r * 96 + c];
+    for (int u = w * 32; u < end; ++u) {
         const unsigned p = (unsigned)gn[u];
-        float* e = entry(dense, p, p);
+        if (p != cur) {
+            float* e = entry(dense, cur, cur);
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
+            cur = p;
+            e = entry(dense, cur, cur);
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
+        }
         const float* a = od + 9 * (size_t)u;
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], a[r * 3 + c]);
+        for (int e = 0; e < 9; ++e) acc[e] = __fadd_rn(acc[e], a[e]);
     }
+    float* e = entry(dense, cur, cur);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
 }
 
 // Stable grouping boundaries: off[key] = first sorted position of key.
@@ -518,14 +564,17 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     float* dense = P<float>(h->dense);
     float* add = P<float>(h->additional);
     const int* gn = P<int>(h->goingNext);
-    const int begin1 = h->levelSize[3];
     // privatize the top level's targets when it is one block (k_collision_hessian)
     const int topNode = (L > 1 && ceil32(h->levelSize[2 * (L - 1)]) == 32) ? h->levelSize[2 * (L - 1) + 1] : -1;
     const int gContact = std::max(1, std::min(kContactBlocks, cdiv(h->nStencil, kContactThreads)));
     if (h->nStencil) {
         k_collision_hessian<<<gContact, kContactThreads, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
                                                                  kContactAdditional, gn, L, topNode, dense, add);
-        if (tc > begin1) k_coarse_additional<<<cdiv(tc - begin1, 256), 256, 0, s>>>(begin1, tc, gn, add, dense);
+        for (int l = 1; l < L; ++l)  // child level l: own diagonals (l = 1), then S into level l + 1 (< L)
+            if (l == 1 || l + 1 < L)
+                k_additional_up<<<cdiv(h->levelSize[2 * l], 64), 64, 0, s>>>(h->levelSize[2 * l + 1],
+                                                                             h->levelSize[2 * l], tc, l == 1, gn,
+                                                                             add, dense);
     }
     k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
                                               d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt));
