@@ -39,6 +39,8 @@
 
 namespace mas {
 
+static int bit_width(unsigned x) { return x ? 32 - __builtin_clz(x) : 0; }
+
 struct EdgeRec {
     int lam;  // first common-bank level, 1..L-1
     int row;  // anc_lam(u) (global node id)
@@ -298,7 +300,21 @@ __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* _
     for (int q = lane; q < kDenseFloats / 4; q += 64) gblk[q] = t4[q];
 }
 
-__global__ __launch_bounds__(256) void k_records(int nV, int L, const int* __restrict__ s2o,
+// Record keys pack (row, col) as coarse ids relative to level 1 in B bits each
+// (B = bit width of the coarse node count, 16 at 1M): the stable radix sort
+// then runs over 2B bits instead of 64 (4 passes instead of 8 at 1M).  A dead
+// record's key has all 2B bits set, above every live key (ids < 2^B - 1).
+struct RecKey {
+    int begin1, B;
+    __device__ unsigned long long dead() const { return (1ull << (2 * B)) - 1; }
+    __device__ unsigned long long pack(unsigned row, unsigned col) const {
+        return ((unsigned long long)(row - begin1) << B) | (col - begin1);
+    }
+    __device__ unsigned row(unsigned long long k) const { return (unsigned)(k >> B) + begin1; }
+    __device__ unsigned col(unsigned long long k) const { return (unsigned)(k & ((1ull << B) - 1)) + begin1; }
+};
+
+__global__ __launch_bounds__(256) void k_records(int nV, int L, RecKey rk, const int* __restrict__ s2o,
                                                  const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                  const int* __restrict__ gn, const int* __restrict__ ranges,
                                                  const int* __restrict__ recOff, EdgeRec* __restrict__ rec,
@@ -315,10 +331,10 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, const int* __res
         const int level = climb(gn, L, my, ot);
         if (level >= L) {  // no common bank below L (.cpp:1286): a dead record, sorted last
             rec[w] = EdgeRec{L, -1, -1, base + k - 1};
-            keys[w] = ~0ull;
+            keys[w] = rk.dead();
         } else {
             rec[w] = EdgeRec{level, (int)my, (int)ot, base + k - 1};
-            keys[w] = ((unsigned long long)my << 32) | ot;
+            keys[w] = rk.pack(my, ot);
         }
         mats[w] = base + k - 1;  // sort payload: records of one entry stay in (u, k) order (stable sort)
         ++w;
@@ -342,15 +358,15 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, const int* __res
 // atomics on one address serialised and cost ~300 us.)
 constexpr int kLongRun = 16, kFoldBatch = 8;
 
-__global__ __launch_bounds__(256) void k_fold_entries(int n, const unsigned long long* __restrict__ keys,
+__global__ __launch_bounds__(256) void k_fold_entries(int n, RecKey rk, const unsigned long long* __restrict__ keys,
                                                       const int* __restrict__ mats, const float* __restrict__ off9,
                                                       float* __restrict__ dense) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const unsigned long long key = keys[i];
-    if (key == ~0ull || (i > 0 && keys[i - 1] == key)) return;
+    if (key == rk.dead() || (i > 0 && keys[i - 1] == key)) return;
     if (i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key) return;  // sorted: >= kLongRun records, k_fold_long
-    float* e = entry(dense, (unsigned)(key >> 32), (unsigned)(key & 0xffffffffu));
+    float* e = entry(dense, rk.row(key), rk.col(key));
     float acc[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
@@ -376,7 +392,7 @@ __global__ __launch_bounds__(256) void k_fold_entries(int n, const unsigned long
         for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
 }
 
-__global__ __launch_bounds__(64) void k_fold_long(int n, const unsigned long long* __restrict__ keys,
+__global__ __launch_bounds__(64) void k_fold_long(int n, RecKey rk, const unsigned long long* __restrict__ keys,
                                                   const int* __restrict__ mats, const float* __restrict__ off9,
                                                   float* __restrict__ dense) {
     __shared__ float T[9 * 65];  // T[q * 65 + record]: off9 component q; stride 65 keeps lanes 0..8 on distinct banks
@@ -386,12 +402,12 @@ __global__ __launch_bounds__(64) void k_fold_long(int n, const unsigned long lon
     bool isLong = false;
     if (i < n) {
         const unsigned long long key = keys[i];
-        isLong = key != ~0ull && (i == 0 || keys[i - 1] != key) && i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key;
+        isLong = key != rk.dead() && (i == 0 || keys[i - 1] != key) && i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key;
     }
     for (unsigned long long starts = __ballot(isLong); starts; starts &= starts - 1) {
         const int start = blockIdx.x * 64 + __ffsll((long long)starts) - 1;
         const unsigned long long key = keys[start];
-        float* e = entry(dense, (unsigned)(key >> 32), (unsigned)(key & 0xffffffffu));
+        float* e = entry(dense, rk.row(key), rk.col(key));
         float acc = lane < 9 ? e[r * 96 + c] : 0.f;
         for (int j0 = start;; j0 += 64) {
             const int j = j0 + lane;
@@ -601,25 +617,26 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         (rc = ensure(h, h->recIdsSorted, nr * 4)))
         return rc;
     EdgeRec* rec = P<EdgeRec>(h->rec);
-    k_records<<<cdiv(nV, 256), 256, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), gn, d_ranges,
+    const RecKey rk{h->levelSize[3], bit_width((unsigned)(tc - h->levelSize[3]))};
+    k_records<<<cdiv(nV, 256), 256, 0, s>>>(nV, L, rk, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), gn, d_ranges,
                                             P<int>(h->recOff), rec, P<unsigned long long>(h->recKeys),
                                             P<int>(h->recIds));
     if (nRec > 0) {
         tmp = 0;
         hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, P<unsigned long long>(h->recKeys),
                                            P<unsigned long long>(h->recKeysSorted), P<int>(h->recIds),
-                                           P<int>(h->recIdsSorted), nRec, 0, 64, s);
+                                           P<int>(h->recIdsSorted), nRec, 0, 2 * rk.B, s);
         if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
         if ((rc = hip_check(h,
                             hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, P<unsigned long long>(h->recKeys),
                                                                P<unsigned long long>(h->recKeysSorted),
                                                                P<int>(h->recIds), P<int>(h->recIdsSorted), nRec, 0,
-                                                               64, s),
+                                                               2 * rk.B, s),
                             "record sort")))
             return rc;
-        k_fold_entries<<<cdiv(nRec, 256), 256, 0, s>>>(nRec, P<unsigned long long>(h->recKeysSorted),
+        k_fold_entries<<<cdiv(nRec, 256), 256, 0, s>>>(nRec, rk, P<unsigned long long>(h->recKeysSorted),
                                                        P<int>(h->recIdsSorted), d_off9, dense);
-        k_fold_long<<<cdiv(nRec, 64), 64, 0, s>>>(nRec, P<unsigned long long>(h->recKeysSorted),
+        k_fold_long<<<cdiv(nRec, 64), 64, 0, s>>>(nRec, rk, P<unsigned long long>(h->recKeysSorted),
                                                   P<int>(h->recIdsSorted), d_off9, dense);
     }
     k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
@@ -635,12 +652,14 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         const int* cstPrev = P<int>(h->cst) + (size_t)(l - 1) * nV;  // level-l local id per vertex
         const int* cstPrev2 = P<int>(h->cst) + (size_t)(l - 2) * nV; // level-(l-1) local id per vertex
         tmp = 0;
+        // keys are level-l local ids < count: sort only their bits
+        const int vbits = std::max(1, bit_width((unsigned)std::max(count - 1, 0)));
         hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, cstPrev, P<int>(h->vkeys), P<int>(h->iota), P<int>(h->vlist),
-                                           nV, 0, 32, s);
+                                           nV, 0, vbits, s);
         if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
         if ((rc = hip_check(h,
                             hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, cstPrev, P<int>(h->vkeys),
-                                                               P<int>(h->iota), P<int>(h->vlist), nV, 0, 32, s),
+                                                               P<int>(h->iota), P<int>(h->vlist), nV, 0, vbits, s),
                             "vertex-list sort")))
             return rc;
         k_bounds<<<cdiv(nV, 256), 256, 0, s>>>(nV, P<int>(h->vkeys), count, P<int>(h->voff));
