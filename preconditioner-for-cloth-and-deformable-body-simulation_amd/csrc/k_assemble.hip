@@ -87,9 +87,16 @@ constexpr int kContactThreads = 1024, kContactBlocks = 256;
 // nodes' additional terms): 10.8 M same-address float atomics for 100k VF
 // contacts, 0.6 ms per pass.  When the top level is one block, each
 // workgroup therefore accumulates those targets in LDS (LDS float atomics)
-// and adds its partial sums to HBM once at the end -- 64 workgroups, so 64
-// global adds per target.  Other targets are added directly as before.  Sums
-// of contact terms are atomic (order-free) in the reference too (B-10).
+// and adds its partial sums to HBM once at the end (kContactBlocks
+// workgroups, so that many global adds per target).  Other targets are added
+// directly.  Sums of contact terms are atomic (order-free) in the reference
+// too (B-10).
+// Sixteen lanes per stencil, lane e < 9 owning entry (e / 3, e % 3) of every
+// 3x3 term: a wave's atomic instruction then covers 4 targets x 9 floats in
+// 12-36-byte runs.  With a thread per stencil each instruction sent 64 lanes
+// to 64 different cache lines, the slowest shape of global atomics (~17x below
+// contiguous, MI355X_MICROARCH.md atomics table): 341 us per pass at 100k VF.
+constexpr int kLanesPerStencil = 16;
 __global__ __launch_bounds__(kContactThreads) void k_collision_hessian(const DevStencil* __restrict__ st, int n,
                                                                        int mode, const int* __restrict__ gn, int L,
                                                                        int topNode, float* __restrict__ dense,
@@ -101,68 +108,45 @@ __global__ __launch_bounds__(kContactThreads) void k_collision_hessian(const Dev
     if (privatize)
         for (int e = threadIdx.x; e < nPriv; e += blockDim.x) priv[e] = 0.f;
     __syncthreads();
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const DevStencil s = st[i];
-        float ds[3] = {__fmul_rn(s.dir[0], s.stiff), __fmul_rn(s.dir[1], s.stiff), __fmul_rn(s.dir[2], s.stiff)};
-        float hm[3][3];  // OuterProduct(d, d * stiff), SeMatrix.h:352-363
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) hm[r][c] = __fmul_rn(s.dir[r], ds[c]);
-        for (int it = 0; mode == kContactAdditional && it < s.n; ++it) {  // .cpp:1214-1217: additional[idx] += h w^2
-            const float w2 = __fmul_rn(s.w[it], s.w[it]);
-            float* a = additional + 9 * (size_t)s.idx[it];
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) atomicAdd(a + r * 3 + c, __fmul_rn(hm[r][c], w2));
-        }
+    const int e = threadIdx.x % kLanesPerStencil, r = e / 3, c = e % 3;
+    const int perGrid = gridDim.x * (blockDim.x / kLanesPerStencil);
+    for (int i = blockIdx.x * (blockDim.x / kLanesPerStencil) + threadIdx.x / kLanesPerStencil; i < n; i += perGrid) {
+        if (e >= 9) continue;
+        const DevStencil& s = st[i];  // read in place: a private copy indexed by it/a/b would live in scratch
+        // OuterProduct(d, d * stiff), SeMatrix.h:352-363: entry (r, c) = d_r (d_c stiff)
+        const float hm = __fmul_rn(s.dir[r], __fmul_rn(s.dir[c], s.stiff));
+        for (int it = 0; mode == kContactAdditional && it < s.n; ++it)  // .cpp:1214-1217: additional[idx] += h w^2
+            atomicAdd(additional + 9 * (size_t)s.idx[it] + e, __fmul_rn(hm, __fmul_rn(s.w[it], s.w[it])));
         for (int a = 0; a < s.n; ++a)  // AdditionalSchwarzHessian2, .cpp:1164-1199
             for (int b = a + 1; b < s.n; ++b) {
-                const float ww = __fmul_rn(s.w[a], s.w[b]);
+                const float t = __fmul_rn(__fmul_rn(s.w[a], s.w[b]), hm);
                 unsigned my = (unsigned)s.idx[a], ot = (unsigned)s.idx[b];
                 const int level = climb(gn, L, my, ot);
                 if (level >= L) continue;
                 // LDS and HBM targets on separate paths: one pointer that may be
                 // either compiles to flat atomics, which serialise on LDS
                 if (mode == kContactPairs) {
-                    float t[9];
-                    for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e / 3][e % 3]);
                     if ((my >> 5) == topBank) {
-                        const int o0 = (3 * (my & 31)) * 96 + 3 * (ot & 31), o1 = (3 * (ot & 31)) * 96 + 3 * (my & 31);
-                        for (int e = 0; e < 9; ++e) {
-                            atomicAdd(&priv[o0 + (e / 3) * 96 + e % 3], t[e]);
-                            atomicAdd(&priv[o1 + (e / 3) * 96 + e % 3], t[e]);
-                        }
+                        atomicAdd(&priv[(3 * (my & 31) + r) * 96 + 3 * (ot & 31) + c], t);
+                        atomicAdd(&priv[(3 * (ot & 31) + r) * 96 + 3 * (my & 31) + c], t);
                     } else {
-                        float* e0 = entry(dense, my, ot);
-                        float* e1 = entry(dense, ot, my);
-                        for (int e = 0; e < 9; ++e) {
-                            atomicAdd(e0 + (e / 3) * 96 + e % 3, t[e]);
-                            atomicAdd(e1 + (e / 3) * 96 + e % 3, t[e]);
-                        }
+                        atomicAdd(entry(dense, my, ot) + r * 96 + c, t);
+                        atomicAdd(entry(dense, ot, my) + r * 96 + c, t);
                     }
                 } else if (level < L - 1) {
                     const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
-                    float t[9];
-                    for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e / 3][e % 3]);
                     if ((pm >> 5) == topBank) {  // then po is a top node too
-                        const int om = 9 * (pm & 31), oo = 9 * (po & 31);
-                        for (int e = 0; e < 9; ++e) {
-                            if (pm == po) {
-                                atomicAdd(&priv[om + e], __fmul_rn(t[e], 2.0f));
-                            } else {
-                                atomicAdd(&priv[om + e], t[e]);
-                                atomicAdd(&priv[oo + e], t[e]);
-                            }
+                        if (pm == po) {
+                            atomicAdd(&priv[9 * (pm & 31) + e], __fmul_rn(t, 2.0f));
+                        } else {
+                            atomicAdd(&priv[9 * (pm & 31) + e], t);
+                            atomicAdd(&priv[9 * (po & 31) + e], t);
                         }
+                    } else if (pm == po) {
+                        atomicAdd(additional + 9 * (size_t)pm + e, __fmul_rn(t, 2.0f));
                     } else {
-                        float* am = additional + 9 * (size_t)pm;
-                        float* ao = additional + 9 * (size_t)po;
-                        for (int e = 0; e < 9; ++e) {
-                            if (pm == po) {
-                                atomicAdd(am + e, __fmul_rn(t[e], 2.0f));
-                            } else {
-                                atomicAdd(am + e, t[e]);
-                                atomicAdd(ao + e, t[e]);
-                            }
-                        }
+                        atomicAdd(additional + 9 * (size_t)pm + e, t);
+                        atomicAdd(additional + 9 * (size_t)po + e, t);
                     }
                 }
             }
@@ -170,8 +154,8 @@ __global__ __launch_bounds__(kContactThreads) void k_collision_hessian(const Dev
     if (!privatize) return;
     __syncthreads();
     float* dst = mode == kContactPairs ? dense + (size_t)topBank * kDenseFloats : additional + 9 * (size_t)(topBank * 32);
-    for (int e = threadIdx.x; e < nPriv; e += blockDim.x)
-        if (priv[e] != 0.f) atomicAdd(dst + e, priv[e]);
+    for (int q = threadIdx.x; q < nPriv; q += blockDim.x)
+        if (priv[q] != 0.f) atomicAdd(dst + q, priv[q]);
 }
 
 // .cpp:1236-1252: coarse additional -> own diagonal and every ancestor.
@@ -236,7 +220,9 @@ __global__ __launch_bounds__(64) void k_additional_up(int beginC, int nC, int tc
 // and no read-modify-write of scattered 3x3 entries (k_level0 moved 5 GB per
 // launch at 1M for 1.2 GB of blocks as a thread-per-vertex kernel).  The tile
 // starts from zeros; contact pair terms are added afterwards (see
-// k_collision_hessian).
+// k_collision_hessian).  Measured alternative: no LDS, the wave stores the
+// zero block, drains, then each lane stores its 3x3 entries straight to HBM --
+// 749 vs 338 us at 1M (the 12-byte scattered stores are partial-line writes).
 __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* __restrict__ s2o,
                                                      const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                      const float* __restrict__ diag9,
@@ -582,7 +568,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     const int* gn = P<int>(h->goingNext);
     // privatize the top level's targets when it is one block (k_collision_hessian)
     const int topNode = (L > 1 && ceil32(h->levelSize[2 * (L - 1)]) == 32) ? h->levelSize[2 * (L - 1) + 1] : -1;
-    const int gContact = std::max(1, std::min(kContactBlocks, cdiv(h->nStencil, kContactThreads)));
+    const int gContact =
+        std::max(1, std::min(kContactBlocks, cdiv(h->nStencil, kContactThreads / kLanesPerStencil)));
     if (h->nStencil) {
         k_collision_hessian<<<gContact, kContactThreads, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
                                                                  kContactAdditional, gn, L, topNode, dense, add);
