@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256) void k_term_write(int l, int nV, const int* __
     if (l == 2) terms[o] = -(u + 1);
 }
 
-constexpr int kFoldChunk = 256;
+constexpr int kFoldChunk = 512, kFoldStride = kFoldChunk + 4;
 
 __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, int beginPrev,
                                                    const int* __restrict__ vlist, const int* __restrict__ voff,
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, 
                                                    const int* __restrict__ cstPrev2, const int* __restrict__ gn,
                                                    const float* __restrict__ off9, const float* __restrict__ od,
                                                    float* __restrict__ tab, float* __restrict__ dense) {
-    __shared__ float st[kFoldChunk * 9];
+    __shared__ __attribute__((aligned(16))) float st[9 * kFoldStride];
     const int local = blockIdx.x;
     const int lane = threadIdx.x;
     const int P = begin + local;
@@ -509,34 +509,83 @@ __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, 
     // lane q < 9 folds entry q = (row, col) = (q / 3, q % 3); off9 is column-major
     const int q = lane < 9 ? lane : 0;
     float acc = 0.f;
+    // Software-pipelined two chunks deep: while lanes 0..8 fold chunk i from
+    // LDS, the term matrices of chunk i+1 (whose term ids arrived during the
+    // previous fold) and the term ids of chunk i+2 are in flight, so no HBM
+    // latency is exposed per chunk (the first form waited two dependent
+    // latencies per 256 terms: 220 us for the ~10k-term chains of the 32
+    // level-3 nodes at 1M).  Loads are unconditional (indices clamped into the
+    // chunk; the fold never reads past n).  LDS is entry-major with a padded
+    // stride, so a folding lane reads 4 terms per ds_read_b128 and lanes 0..8
+    // hit distinct banks.  One wave per workgroup: its LDS operations run in
+    // program order and one buffer suffices.
+    constexpr int kPer = kFoldChunk / 64;
+    float reg[kPer][9];
+    int tk[kPer];
+    auto loadIds = [&](int base) {
+        const int last = min(kFoldChunk, te - base) - 1;
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) tk[m] = terms[base + min(m * 64 + lane, last)];
+    };
+    auto loadMats = [&]() {
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) {
+            const int t = tk[m];
+            const bool colMajor = t >= 0;
+            const float* src = colMajor ? off9 + 9 * (size_t)t : od + 9 * (size_t)(-t - 1);
+#pragma unroll
+            for (int e = 0; e < 9; ++e) reg[m][e] = src[colMajor ? (e % 3) * 3 + e / 3 : e];
+        }
+    };
+    if (tb < te) {
+        loadIds(tb);
+        loadMats();
+        if (tb + kFoldChunk < te) loadIds(tb + kFoldChunk);
+    }
     for (int base = tb; base < te; base += kFoldChunk) {
         const int n = min(kFoldChunk, te - base);
 #pragma unroll
-        for (int m = 0; m < kFoldChunk / 64; ++m) {
-            const int k = m * 64 + lane;
-            if (k < n) {
-                const int t = terms[base + k];
-                const float* src = t >= 0 ? off9 + 9 * (size_t)t : od + 9 * (size_t)(-t - 1);
-                const bool colMajor = t >= 0;
+        for (int m = 0; m < kPer; ++m)
 #pragma unroll
-                for (int e = 0; e < 9; ++e) st[k * 9 + e] = src[colMajor ? (e % 3) * 3 + e / 3 : e];
-            }
-        }
+            for (int e = 0; e < 9; ++e) st[e * kFoldStride + m * 64 + lane] = reg[m][e];
         __syncthreads();
-        if (lane < 9)
-            for (int k = 0; k < n; ++k) acc = __fadd_rn(acc, st[k * 9 + q]);
+        if (base + kFoldChunk < te) {
+            loadMats();
+            if (base + 2 * kFoldChunk < te) loadIds(base + 2 * kFoldChunk);
+        }
+        if (lane < 9) {
+            const float* col = st + q * kFoldStride;
+            int k = 0;
+            for (; k + 8 <= n; k += 8) {
+                const float4 x0 = *reinterpret_cast<const float4*>(col + k);
+                const float4 x1 = *reinterpret_cast<const float4*>(col + k + 4);
+                acc = __fadd_rn(acc, x0.x);
+                acc = __fadd_rn(acc, x0.y);
+                acc = __fadd_rn(acc, x0.z);
+                acc = __fadd_rn(acc, x0.w);
+                acc = __fadd_rn(acc, x1.x);
+                acc = __fadd_rn(acc, x1.y);
+                acc = __fadd_rn(acc, x1.z);
+                acc = __fadd_rn(acc, x1.w);
+            }
+            for (; k < n; ++k) acc = __fadd_rn(acc, col[k]);
+        }
         __syncthreads();
     }
     bool present = te > tb;
     if (l >= 3 && ve > vb) {  // pushes of the level-(l-1) tables, children in id order (.cpp:1333-1341)
         const int childLocal = cstPrev2[vlist[vb]];  // level-(l-1) local id of the first member
         const int bankBase = beginPrev + (childLocal & ~31);
-        for (int j = 0; j < 32; ++j) {
-            const int c = bankBase + j;
-            if (gn[c] != P) continue;
-            if (lane < 9) acc = __fadd_rn(acc, tab[9 * (size_t)c + q]);
-            present = true;
+        // the bank's 32 parent ids and all 288 table floats are loaded at once
+        // (a dependent load per child cost ~32 HBM latencies per node)
+        const unsigned long long kids = __ballot(lane < 32 && gn[bankBase + (lane & 31)] == P) & 0xffffffffull;
+        for (int x = lane; x < 32 * 9; x += 64) st[x] = tab[9 * (size_t)bankBase + x];
+        __syncthreads();
+        for (unsigned long long m = kids; m; m &= m - 1) {
+            const int j = __ffsll((long long)m) - 1;  // children in id order
+            if (lane < 9) acc = __fadd_rn(acc, st[9 * j + q]);
         }
+        present = present || kids != 0;
     }
     if (lane < 9) {
         tab[9 * (size_t)P + q] = acc;
