@@ -33,6 +33,10 @@ namespace mas {
 // so the r gather is the second dependent load.  128-thread workgroups spread
 // the 512 waves (1M) over the CUs.
 constexpr int kRestrictWaves = 2;  // waves per workgroup (1 measured 8.4 vs 8.1 us at 1M)
+// Measured, not adopted: one wave per bank solving its level-1 block right
+// here (record loaded beside the gathers, k_solve123 left with levels 2-3):
+// 12.5 + 5.2 us vs 8.1 + 7.9 us -- 244 VGPRs and the gather chain in front of
+// the solve make the fused wave slower than two short launches.
 
 __global__ __launch_bounds__(64 * kRestrictWaves) void k_restrict12(int n1, int begin1, const int* __restrict__ l1src,
                                                     const int* __restrict__ goingNext,
