@@ -110,6 +110,82 @@ __device__ __forceinline__ void spmv_rows(int base, int nV, int lane, const int*
 }
 constexpr int kSpmvRows = 4;  // row groups per wave and pass
 
+// The SpMV's CSR blocks in wave-slot ELL form, built once per solve: a group
+// of 64/G consecutive rows is one wave-row of 64 slots (slot = row-in-group *
+// G + j, j = the row's j-th CSR entry, j < G), stored component-major:
+// ellOff[group * 576 + q * 64 + slot] = off9[9 e + q], ellIdx[group * 64 +
+// slot] = idx[e] (-1: no entry).  Each of a lane's nine off loads is then one
+// 256-byte coalesced wave access instead of a 36-byte-strided sweep (the CSR
+// form's 64 lanes x 36 B span 18 cache lines per instruction), and the idx
+// load no longer waits for starts.  Entries j >= G (rows longer than G) stay
+// in the CSR arrays.  Same entries on the same lanes in the same order:
+// bitwise equal to the CSR form.
+template <int G>
+__global__ __launch_bounds__(256) void k_pcg_ell(int nV, int nGroups, const int* __restrict__ starts,
+                                                 const int* __restrict__ idx, const float* __restrict__ off,
+                                                 float* __restrict__ ellOff, int* __restrict__ ellIdx) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nGroups * 64) return;
+    const int gi = t >> 6, slot = t & 63;
+    const int v = gi * (64 / G) + slot / G, j = slot % G;
+    int e = -1;
+    if (v < nV) {
+        const int e0 = starts[v] + j;
+        if (e0 < starts[v + 1]) e = e0;
+    }
+    ellIdx[t] = e >= 0 ? idx[e] : -1;
+    float* dst = ellOff + (size_t)gi * 576 + slot;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) dst[q * 64] = e >= 0 ? off[9 * (size_t)e + q] : 0.f;
+}
+
+// spmv_rows on the ELL form (base is a multiple of 64/G: XcdRows deals whole
+// row groups)
+template <int G, int R>
+__device__ __forceinline__ void spmv_rows_ell(int base, int nV, int lane, const int* __restrict__ starts,
+                                              const int* __restrict__ idx, const float* __restrict__ diag,
+                                              const float* __restrict__ off, const float* __restrict__ ellOff,
+                                              const int* __restrict__ ellIdx, const float4* __restrict__ x,
+                                              int (&v)[R], float3 (&acc)[R]) {
+    const int sub = lane % G;
+    const int g0 = base / (64 / G);
+    int e[R], e1[R], nb[R];
+    float m[R][9];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        v[r] = base + r * (64 / G) + lane / G;
+        nb[r] = ellIdx[(size_t)(g0 + r) * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) m[r][q] = ellOff[(size_t)(g0 + r) * 576 + q * 64 + lane];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {  // only rows longer than G read the CSR arrays
+        const bool valid = v[r] < nV;
+        e[r] = valid ? starts[v[r]] + sub : 0;
+        e1[r] = valid ? starts[v[r] + 1] : 0;
+    }
+    float4 xn[R], xd[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        xn[r] = x[nb[r] >= 0 ? nb[r] : 0];
+        xd[r] = x[v[r] < nV ? v[r] : 0];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        acc[r] = make_float3(0.f, 0.f, 0.f);
+        if (sub == 0 && v[r] < nV) acc[r] = mat3_mul(diag + 9 * (size_t)v[r], xd[r]);
+        if (nb[r] >= 0) add3(acc[r], mat3_mul(m[r], xn[r]));
+        for (int ee = e[r] + G; ee < e1[r]; ee += G) add3(acc[r], mat3_mul(off + 9 * (size_t)ee, x[idx[ee]]));
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) {
+            acc[r].x = __fadd_rn(acc[r].x, __shfl_xor(acc[r].x, o));
+            acc[r].y = __fadd_rn(acc[r].y, __shfl_xor(acc[r].y, o));
+            acc[r].z = __fadd_rn(acc[r].z, __shfl_xor(acc[r].z, o));
+        }
+    }
+}
+
+
 // XCD-aware row ranges: workgroups are dealt round-robin over the 8 XCDs
 // (b and b + 8 share one; speed only, never correctness), so workgroups
 // b % 8 == k sweep the k-th contiguous eighth of the rows.  A row's
@@ -220,7 +296,9 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_true_finish(const double* _
 template <int G>
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __restrict__ starts,
                                                           const int* __restrict__ idx, const float* __restrict__ diag,
-                                                          const float* __restrict__ off, const float4* __restrict__ p,
+                                                          const float* __restrict__ off,
+                                                          const float* __restrict__ ellOff,
+                                                          const int* __restrict__ ellIdx, const float4* __restrict__ p,
                                                           float4* __restrict__ ap, const PcgState* __restrict__ st,
                                                           double* __restrict__ part) {
     if (st->done) return;
@@ -231,7 +309,7 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __r
     for (int base = xr.first; base < xr.end; base += xr.stride) {
         int v[kSpmvRows];
         float3 y[kSpmvRows];
-        spmv_rows<G, kSpmvRows>(base, nV, lane, starts, idx, diag, off, p, v, y);
+        spmv_rows_ell<G, kSpmvRows>(base, nV, lane, starts, idx, diag, off, ellOff, ellIdx, p, v, y);
 #pragma unroll
         for (int q = 0; q < kSpmvRows; ++q) {
             if (sub == 0 && v[q] < nV) {
@@ -332,6 +410,13 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     const int* idx = P<int>(h->idx);
     const dim3 g(kPcgBlocks), b(kPcgThreads);
     int rc;
+    const int nGroups = cdiv(nV, 64 / G);
+    if ((rc = ensure(h, h->pcgEllOff, (size_t)nGroups * 576 * 4)) ||
+        (rc = ensure(h, h->pcgEllIdx, (size_t)nGroups * 64 * 4)))
+        return rc;
+    float* ellOff = P<float>(h->pcgEllOff);
+    int* ellIdx = P<int>(h->pcgEllIdx);
+    k_pcg_ell<G><<<cdiv(nGroups * 64, 256), 256, 0, s>>>(nV, nGroups, d_ranges, idx, d_off9, ellOff, ellIdx);
     k_pcg_residual<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, r, part);
     k_pcg_start<<<1, b, 0, s>>>(part, st);
     if (precondition) {
@@ -344,7 +429,7 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     const int chunk = 4;
     for (int it = 0; it < maxIters; it += chunk) {
         for (int k = it; k < it + chunk && k < maxIters; ++k) {
-            k_pcg_spmv<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, p, ap, st, part);
+            k_pcg_spmv<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, p, ap, st, part);
             k_pcg_update_xr<<<g, b, 0, s>>>(nV, k, p, ap, d_x, r, st, part);
             if (precondition) {
                 if ((rc = run_apply(h, z, r, s))) return rc;

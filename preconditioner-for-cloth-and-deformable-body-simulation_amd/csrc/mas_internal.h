@@ -85,6 +85,7 @@ struct mas_context {
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, shardPos1, l1src;
     mas::Buffer chainPrange, chainNeed, chainCnt;  // one-launch coarse chain (k_coarse_chain.hip)
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
+    mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
     std::vector<int> l1First;  // first level-1 local id per level-0 bank (+ n1), for sharding
     int shardWorld = 0;
     hipEvent_t* shardPendingEv = nullptr;  // profiling events of an overlapped sharded apply in flight
@@ -106,7 +107,7 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &tileSlot, &valuSlot, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
