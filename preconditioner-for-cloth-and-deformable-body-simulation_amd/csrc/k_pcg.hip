@@ -410,7 +410,10 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     const int* idx = P<int>(h->idx);
     const dim3 g(kPcgBlocks), b(kPcgThreads);
     int rc;
-    const int nGroups = cdiv(nV, 64 / G);
+    // a pass reads kSpmvRows whole groups from a group-aligned base < nV, so
+    // the last pass may read up to kSpmvRows - 1 groups past the rows: they
+    // are allocated and filled as empty slots (idx -1)
+    const int nGroups = cdiv(nV, 64 / G) + kSpmvRows;
     if ((rc = ensure(h, h->pcgEllOff, (size_t)nGroups * 576 * 4)) ||
         (rc = ensure(h, h->pcgEllIdx, (size_t)nGroups * 64 * 4)))
         return rc;
