@@ -220,9 +220,10 @@ __global__ __launch_bounds__(64) void k_additional_up(int beginC, int nC, int tc
 // and no read-modify-write of scattered 3x3 entries (k_level0 moved 5 GB per
 // launch at 1M for 1.2 GB of blocks as a thread-per-vertex kernel).  The tile
 // starts from zeros; contact pair terms are added afterwards (see
-// k_collision_hessian).  Measured alternative: no LDS, the wave stores the
+// k_collision_hessian).  Measured alternatives: no LDS, the wave stores the
 // zero block, drains, then each lane stores its 3x3 entries straight to HBM --
-// 749 vs 338 us at 1M (the 12-byte scattered stores are partial-line writes).
+// 749 vs 338 us at 1M (the 12-byte scattered stores are partial-line writes);
+// persistent workgroups (4 per CU) looping over blocks -- 355 us.
 __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* __restrict__ s2o,
                                                      const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                      const float* __restrict__ diag9,
