@@ -20,7 +20,7 @@
 //                 entries (oldDiagonal, .cpp:1270-1298), count of coarse edges
 //   k_records     coarse edges (u, k) with first common-bank level 1..L-1, in
 //                 (u, k) order
-//   k_fold_entries, k_fold_long  per coarse entry (row, col), (key, mat)
+//   k_fold_runs   per coarse entry (row, col), (key, mat)
 //                 pairs sorted stably by key = (row, col): entry += mat in
 //                 (u, k) order (short runs: a thread; long runs: a wave)
 //   k_diag1       one thread per level-0 bank: diag(anc1(u)) += od(u) (.cpp:1309-1312)
@@ -378,71 +378,69 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, RecKey rk, const
 // entry, hundreds per level-3 entry), and a thread walking a long run pays two
 // dependent load latencies per record (mats, then off9) -- the longest runs set
 // the kernel time.  So:
-//   k_fold_entries  one thread per run shorter than kLongRun; records are
-//                 loaded kFoldBatch at a time (all loads issued, then the adds
-//                 in order).
-//   k_fold_long   one wave per 64 sorted positions; it folds, one after the
-//                 other, the runs of kLongRun or more that start there: 64
-//                 records per step are loaded by the lanes into LDS, then lanes
-//                 0..8 each fold one of the nine entries over them in order.
+//   short runs (< kLongRun): one lane each; records are loaded kFoldBatch at
+//                 a time (all loads issued, then the adds in order).
+//   long runs:    the wave, one run after the other: 64 records per step are
+//                 loaded by the lanes into LDS, then lanes 0..8 each fold one
+//                 of the nine entries over them in order.
 // (Collecting the long runs into a list with a counter was measured first: ~60k
 // atomics on one address serialised and cost ~300 us.)
 constexpr int kLongRun = 16, kFoldBatch = 8;
 
-__global__ __launch_bounds__(256) void k_fold_entries(int n, RecKey rk, const unsigned long long* __restrict__ keys,
-                                                      const int* __restrict__ mats, const float* __restrict__ off9,
-                                                      float* __restrict__ dense) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const unsigned long long key = keys[i];
-    if (key == rk.dead() || (i > 0 && keys[i - 1] == key)) return;
-    if (i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key) return;  // sorted: >= kLongRun records, k_fold_long
-    float* e = entry(dense, rk.row(key), rk.col(key));
-    float acc[9];
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
-    for (int j0 = i; j0 < i + kLongRun; j0 += kFoldBatch) {
-        bool in[kFoldBatch];
-        float m[kFoldBatch][9];
-#pragma unroll
-        for (int t = 0; t < kFoldBatch; ++t) {
-            const int j = j0 + t;
-            in[t] = j < n && keys[j] == key;
-            const float* src = off9 + 9 * (size_t)(in[t] ? mats[j] : mats[i]);
-#pragma unroll
-            for (int q = 0; q < 9; ++q) m[t][q] = src[q];
-        }
-#pragma unroll
-        for (int t = 0; t < kFoldBatch; ++t)
-            if (in[t])
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[t][c * 3 + r]);
-        if (!in[kFoldBatch - 1]) break;
-    }
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
-}
-
-__global__ __launch_bounds__(64) void k_fold_long(int n, RecKey rk, const unsigned long long* __restrict__ keys,
+// One wave per 64 sorted positions: the lanes find the runs starting there;
+// each short-run lane folds its own run, then the wave folds the long runs one
+// after the other.  (Separate kernels for the two kinds measured 106 + 78 us
+// at 1M: each re-read the keys to find its runs.)
+__global__ __launch_bounds__(64) void k_fold_runs(int n, RecKey rk, const unsigned long long* __restrict__ keys,
                                                   const int* __restrict__ mats, const float* __restrict__ off9,
                                                   float* __restrict__ dense) {
     __shared__ float T[9 * 65];  // T[q * 65 + record]: off9 component q; stride 65 keeps lanes 0..8 on distinct banks
     const int lane = threadIdx.x;
-    const int r = lane / 3, c = lane % 3;
     const int i = blockIdx.x * 64 + lane;
-    bool isLong = false;
+    bool isStart = false, isLong = false;
+    unsigned long long key = 0;
     if (i < n) {
-        const unsigned long long key = keys[i];
-        isLong = key != rk.dead() && (i == 0 || keys[i - 1] != key) && i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key;
+        key = keys[i];
+        isStart = key != rk.dead() && (i == 0 || keys[i - 1] != key);
+        // sorted: a run starting at i has >= kLongRun records iff position i + kLongRun - 1 has its key
+        isLong = isStart && i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key;
     }
+    if (isStart && !isLong) {  // short run: this lane, loads batched kFoldBatch at a time
+        float* e = entry(dense, rk.row(key), rk.col(key));
+        float acc[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
+        for (int j0 = i; j0 < i + kLongRun; j0 += kFoldBatch) {
+            bool in[kFoldBatch];
+            float m[kFoldBatch][9];
+#pragma unroll
+            for (int t = 0; t < kFoldBatch; ++t) {
+                const int j = j0 + t;
+                in[t] = j < n && keys[j] == key;
+                const float* src = off9 + 9 * (size_t)(in[t] ? mats[j] : mats[i]);
+#pragma unroll
+                for (int q = 0; q < 9; ++q) m[t][q] = src[q];
+            }
+#pragma unroll
+            for (int t = 0; t < kFoldBatch; ++t)
+                if (in[t])
+                    for (int r = 0; r < 3; ++r)
+                        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[t][c * 3 + r]);
+            if (!in[kFoldBatch - 1]) break;
+        }
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
+    }
+    // long runs: the whole wave, 64 records per step staged in LDS, lanes 0..8 fold
+    const int r = lane / 3, c = lane % 3;
     for (unsigned long long starts = __ballot(isLong); starts; starts &= starts - 1) {
         const int start = blockIdx.x * 64 + __ffsll((long long)starts) - 1;
-        const unsigned long long key = keys[start];
-        float* e = entry(dense, rk.row(key), rk.col(key));
+        const unsigned long long lkey = keys[start];
+        float* e = entry(dense, rk.row(lkey), rk.col(lkey));
         float acc = lane < 9 ? e[r * 96 + c] : 0.f;
         for (int j0 = start;; j0 += 64) {
             const int j = j0 + lane;
-            const bool in = j < n && keys[j] == key;
+            const bool in = j < n && keys[j] == lkey;
             const int cnt = __popcll(__ballot(in));  // the run is contiguous: lanes 0..cnt-1
             if (in) {
                 const float* src = off9 + 9 * (size_t)mats[j];
@@ -732,9 +730,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                                                                2 * rk.B, s),
                             "record sort")))
             return rc;
-        k_fold_entries<<<cdiv(nRec, 256), 256, 0, s>>>(nRec, rk, P<unsigned long long>(h->recKeysSorted),
-                                                       P<int>(h->recIdsSorted), d_off9, dense);
-        k_fold_long<<<cdiv(nRec, 64), 64, 0, s>>>(nRec, rk, P<unsigned long long>(h->recKeysSorted),
+        k_fold_runs<<<cdiv(nRec, 64), 64, 0, s>>>(nRec, rk, P<unsigned long long>(h->recKeysSorted),
                                                   P<int>(h->recIdsSorted), d_off9, dense);
     }
     k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
