@@ -22,10 +22,19 @@ namespace mas {
 
 // flag[i]: 1 = valid record, 0 = skipped (negative id, .cpp:330,359,385),
 // 2 = id out of range (reference UB; reported as MAS_ERR_ARG).
+// flag[i] = 1 for a record that becomes a stencil, 0 otherwise (flag[total]
+// = 0 closes the scan); a record naming an out-of-range edge/face/vertex sets
+// *bad, which the host reads with the stencil count (one 8-byte copy, not the
+// whole flag array: that copy and a host pass over it cost ~115 us at 100k).
 __global__ __launch_bounds__(256) void k_stencil_flags(const unsigned char* __restrict__ raw, int efNum, int eeNum,
-                                                       int total, int nV, int nE, int nF, int* __restrict__ flag) {
+                                                       int total, int nV, int nE, int nF, int* __restrict__ flag,
+                                                       int* __restrict__ bad) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
+    if (i > total) return;
+    if (i == total) {
+        flag[i] = 0;
+        return;
+    }
     const int* rec = reinterpret_cast<const int*>(raw + 48 * (size_t)i);
     int a = rec[0], b = rec[1];
     int f = 1;
@@ -33,7 +42,8 @@ __global__ __launch_bounds__(256) void k_stencil_flags(const unsigned char* __re
     else if (i < efNum) f = (a < nE && b < nF) ? 1 : 2;
     else if (i < efNum + eeNum) f = (a < nE && b < nE) ? 1 : 2;
     else f = (a < nV && b < nF) ? 1 : 2;
-    flag[i] = f;
+    if (f == 2) atomicOr(bad, 1);
+    flag[i] = f == 1;
 }
 
 __global__ __launch_bounds__(256) void k_stencil_build(const unsigned char* __restrict__ raw, int efNum, int eeNum,
@@ -302,7 +312,7 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
         vfNum = total - efNum - eeNum;
     }
     int rc;
-    if ((rc = ensure(h, h->rawContacts, (size_t)total * 48)) || (rc = ensure(h, h->stencilFlags, (size_t)total * 4)) ||
+    if ((rc = ensure(h, h->rawContacts, (size_t)total * 48)) || (rc = ensure(h, h->stencilFlags, (size_t)(total + 1) * 4)) ||
         (rc = ensure(h, h->stencilSlots, (size_t)total * 4 + 16)) ||
         (rc = ensure(h, h->stencils, (size_t)total * sizeof(DevStencil))))
         return rc;
@@ -314,20 +324,18 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
                                  "stage vf")))
         return rc;
     const int n = (int)total;
-    k_stencil_flags<<<cdiv(n, 256), 256, 0, s>>>(raw, (int)efNum, (int)eeNum, n, h->nV, h->nE, h->nF,
-                                                 P<int>(h->stencilFlags));
-    std::vector<int> flags(n);
-    if ((rc = hip_check(h, hipMemcpyAsync(flags.data(), h->stencilFlags.p, (size_t)n * 4, hipMemcpyDeviceToHost, s),
-                        "D2H flags")) ||
-        (rc = hip_check(h, hipStreamSynchronize(s), "flags sync")))
-        return rc;
-    int valid = 0;
-    for (int f : flags) {
-        if (f == 2) return fail(h, MAS_ERR_ARG, "contact record references an out-of-range edge/face/vertex");
-        valid += (f == 1);
-    }
+    int* slots = P<int>(h->stencilSlots);  // [0, n]: exclusive scan of the flags; [n + 1]: the bad-record word
+    if ((rc = hip_check(h, hipMemsetAsync(slots + n + 1, 0, 4, s), "clear bad-record word"))) return rc;
+    k_stencil_flags<<<cdiv(n + 1, 256), 256, 0, s>>>(raw, (int)efNum, (int)eeNum, n, h->nV, h->nE, h->nF,
+                                                     P<int>(h->stencilFlags), slots + n + 1);
     // deterministic compaction == the reference's atomic slot counter at CPU_THREAD_NUM=1
-    if ((rc = scan_counts(h, P<int>(h->stencilFlags), P<int>(h->stencilSlots), n, s))) return rc;
+    if ((rc = scan_counts(h, P<int>(h->stencilFlags), slots, n + 1, s))) return rc;
+    int head[2] = {0, 0};  // stencil count, bad-record word
+    if ((rc = hip_check(h, hipMemcpyAsync(head, slots + n, 8, hipMemcpyDeviceToHost, s), "D2H stencil count")) ||
+        (rc = hip_check(h, hipStreamSynchronize(s), "stencil count sync")))
+        return rc;
+    if (head[1]) return fail(h, MAS_ERR_ARG, "contact record references an out-of-range edge/face/vertex");
+    const int valid = head[0];
     k_stencil_build<<<cdiv(n, 256), 256, 0, s>>>(raw, (int)efNum, (int)eeNum, n, P<int>(h->stencilFlags),
                                                  P<int>(h->stencilSlots), P<int4>(h->edges), P<int4>(h->faces),
                                                  P<int>(h->o2s), h->cfg.fix_vf_bary, P<DevStencil>(h->stencils));

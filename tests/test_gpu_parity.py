@@ -303,3 +303,21 @@ def test_coarse_blocks_bitwise(kind, W, L):
         d = np.abs(P.block_matrix(blk) - o.block_matrix(blk)).max()
         print(f"{kind}{W} L={L}: {len(bad)} of {nblk - nfine} coarse blocks differ, first {blk}, max |diff| {d:.3e}")
     assert not bad
+
+
+def test_contact_records_validated_on_device():
+    """An out-of-range face id fails Prepare loudly (MAS_ERR_ARG), records
+    with negative ids are skipped (as the reference's `a < 0` test), and the
+    stencil count is the number of valid records."""
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(40)
+    vf, vfC = meshgen.vf_contacts(mesh, 300, seed=9)
+    skip = vf.copy()
+    skip["vId"][:7] = -1
+    P = mas_amd.from_mesh(mesh, contacts=(skip, vfC))
+    assert P.info()["num_stencils"] == 300 - 7
+    bad = vf.copy()
+    bad["fId"][123] = mesh.faces.shape[0] + 5
+    with pytest.raises(mas_amd.MasError, match="out-of-range"):
+        mas_amd.from_mesh(mesh, contacts=(bad, vfC))
