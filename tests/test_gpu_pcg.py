@@ -77,6 +77,9 @@ def test_pcg_deterministic_and_device_path():
     b = meshgen.residual(mesh.nV, 3)
     x1, r1 = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=500, tol=TOL)
     x2, r2 = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=500, tol=TOL)
+    # valence 14: the 16-lane SpMV over the ELL copy of the CSR blocks
+    assert r1["converged"], r1
+    assert _true_rel_res(mesh, x1, b) <= 10 * TOL
     np.testing.assert_array_equal(x1, x2)
     assert r1["iterations"] == r2["iterations"]
     dd = torch.from_numpy(np.ascontiguousarray(mesh.diag, np.float32)).cuda()
