@@ -108,7 +108,7 @@ __device__ __forceinline__ void spmv_rows(int base, int nV, int lane, const int*
         }
     }
 }
-constexpr int kSpmvRows = 4;  // row groups per wave and pass
+constexpr int kSpmvRows = 1;  // row groups per wave and pass
 
 // The SpMV's CSR blocks in wave-slot ELL form, built once per solve: a group
 // of 64/G consecutive rows is one wave-row of 64 slots (slot = row-in-group *
