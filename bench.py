@@ -57,22 +57,55 @@ def algorithmic_bytes(info):
     return fine, apply
 
 
-def pmc_traffic_bytes(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (the
-    counters need their own rocprofv3 passes, so they cannot be read live)."""
-    path = os.path.join(REPO, "profiles", "round1", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        for name, v in d.items():
-            if kernel in name:
-                return int(v["corrected_bytes"])
-    except (OSError, ValueError, KeyError):
-        pass
+def _pmc_summary():
+    """The newest committed PMC summary (profiles/round*/pmc_traffic.json)."""
+    rounds = sorted((d for d in os.listdir(os.path.join(REPO, "profiles")) if d.startswith("round")),
+                    key=lambda d: int("".join(c for c in d if c.isdigit()) or 0))
+    for d in reversed(rounds):
+        path = os.path.join(REPO, "profiles", d, "pmc_traffic.json")
+        if os.path.exists(path):
+            return path
     return None
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (the
+    counters need their own rocprofv3 passes, so they cannot be read live),
+    with the commit and workload that pass measured."""
+    path = _pmc_summary()
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        meta = d.get("__meta__", {})
+        for name, v in d.items():
+            if name != "__meta__" and kernel in name:
+                return int(v["corrected_bytes"]), os.path.relpath(path, REPO), meta
+    except (OSError, TypeError, ValueError, KeyError):
+        pass
+    return None, None, {}
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": avail,
+            "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"), "OMP_PLACES": os.environ.get("OMP_PLACES")}
+
+
 def cpu_baseline(mesh, cfg, contacts, r_np, steps):
+    # SURVEY §8(d): threads pinned close (set before the OpenMP runtime loads)
+    os.environ.setdefault("OMP_PROC_BIND", "close")
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from oracle import Oracle  # test infrastructure: the timed CPU baseline only
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or max(1, (os.cpu_count() or 2) - 1)
@@ -91,7 +124,7 @@ def cpu_baseline(mesh, cfg, contacts, r_np, steps):
         z = o.apply(r_np)
         ts.append(time.perf_counter() - t)
     med = statistics.median(ts)
-    return {"value": round(1.0 / med, 3), "unit": "applies/s", "cores": threads, "kind": "port",
+    return {"value": round(1.0 / med, 3), "unit": "applies/s", "cores": threads, "kind": "port", **cpu_info(),
             "sample": f"{cfg['name']} workload, oracle/ CPU restatement (OpenMP, {threads} threads, "
                       f"reference packed layout), median of {steps} applies after 3 warm-up; "
                       f"ms/apply {med * 1e3:.2f}"}, z
@@ -254,6 +287,7 @@ def main():
         L4 = min(info["num_levels"], 4)
         fine_bytes = ((plan["fine_block_end"] - plan["fine_block_begin"]) * BLOCK_BYTES +
                       (plan["vert_end"] - plan["vert_begin"]) * (36 + 4 * (L4 - 1)))
+    traffic = pmc_traffic("k_solve_fine")
     fine_s = st["fine_ms_avg"] / 1e3
     achieved = fine_bytes / fine_s / 1e9 if fine_s > 0 else None
     value = args.steps / t_max          # applies of the whole problem per second
@@ -298,10 +332,11 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": pmc_traffic_bytes("k_solve_fine"),
-            "traffic_source": "profiles/round1/pmc_traffic.json: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+            "traffic": traffic[0],
+            "traffic_source": f"{traffic[1]}: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                               "passes of this bench command, FETCH_SIZE x2 (gfx950 wide-read correction) + "
                               "WRITE_SIZE, KB = 1024 B, per launch",
+            "traffic_measured_at": traffic[2] or None,
             "bytes_per_launch": fine_bytes,
             "avg_launch_ms": round(st["fine_ms_avg"], 5),
         },

@@ -133,6 +133,66 @@ int blob_save(mas_context* h, void* dst, size_t cap, size_t* written) {
     return MAS_OK;
 }
 
+// Index-map checks of a blob whose checksum matched (FNV-1a detects
+// corruption, not tampering): every id the apply kernels gather through must
+// be in range, so a crafted blob cannot steer a GPU gather out of bounds.
+static bool blob_maps_valid(const MasBlobHeader& hd, const unsigned char* in, const MasBlobSection* sec[]) {
+    const int nV = hd.nV, L = hd.L, tc = hd.totalClusters;
+    const int* ls = hd.levelSize;
+    // level table: level 0 = (nV, 0), begin_{l+1} = begin_l + ceil32(n_l), total = begin_L
+    if (ls[0] != nV || ls[1] != 0) return false;
+    for (int l = 0; l < L; ++l) {
+        const long long n = ls[2 * l], b = ls[2 * l + 1];
+        if (n < 0 || (l > 0 && n > ls[2 * (l - 1)]) || b + (n + 31) / 32 * 32 != ls[2 * (l + 1) + 1]) return false;
+    }
+    if (ls[2 * L + 1] != tc) return false;
+    auto arr = [&](int i) { return reinterpret_cast<const int*>(in + sec[i]->offset); };
+    std::vector<int> seen((size_t)nV, 0);
+    const int* s2o = arr(kSecS2o);
+    const int* o2s = arr(kSecO2s);
+    for (int v = 0; v < nV; ++v) {
+        if (s2o[v] < 0 || s2o[v] >= nV || seen[s2o[v]]++ || o2s[s2o[v]] != v) return false;
+    }
+    const int* gn = arr(kSecGoingNext);
+    for (int i = 0; i < tc; ++i)
+        if (gn[i] < 0 || gn[i] >= tc) return false;
+    const int* cst = arr(kSecCst);
+    for (int l = 0; l < L; ++l)
+        for (int v = 0; v < nV; ++v) {
+            const int c = cst[(size_t)l * nV + v];
+            if (c < 0 || (l + 1 < L && c >= ls[2 * (l + 1)])) return false;
+        }
+    const int* ct = arr(kSecCoarseTables);
+    for (size_t i = 0; i < (size_t)nV * 4; ++i)
+        if (ct[i] < 0 || ct[i] >= tc) return false;
+    // per-vertex apply map {s2o, a1, a2, a3}: ancestors of the prolonged levels
+    const int4* vm = reinterpret_cast<const int4*>(in + sec[kSecVmap]->offset);
+    const int np = L < 4 ? L : 4;
+    for (int v = 0; v < nV; ++v) {
+        const int a[4] = {vm[v].x, vm[v].y, vm[v].z, vm[v].w};
+        if (a[0] != s2o[v]) return false;
+        for (int l = 1; l < np; ++l)
+            if (a[l] < ls[2 * l + 1] || a[l] >= ls[2 * l + 1] + ls[2 * l]) return false;
+    }
+    // coarse members (child bank, component mask): inside the child level
+    const int begin1 = ls[3];
+    const int2* mb = reinterpret_cast<const int2*>(in + sec[kSecMembers]->offset);
+    for (int l = 1; l < L; ++l) {
+        const int nChild = ls[2 * (l - 1)];
+        for (int p = 0; p < (ls[2 * l] + 31) / 32 * 32; ++p) {
+            const int2 m = mb[ls[2 * l + 1] + p - begin1];
+            if (m.x < 0 || (m.y != 0 && 32LL * m.x + 32 - __builtin_clz((unsigned)m.y) > nChild)) return false;
+            if (p >= ls[2 * l] && m.y != 0) return false;  // padding nodes have no children
+        }
+    }
+    // level-1 segment starts per level-0 bank: 0 .. n1, nondecreasing
+    const int* f = arr(kSecL1First);
+    const int n1 = L > 1 ? ls[2] : 0;
+    for (int b = 0; b <= hd.nFineBlk; ++b)
+        if (f[b] < 0 || f[b] > n1 || (b > 0 && f[b] < f[b - 1])) return false;
+    return f[hd.nFineBlk] == n1;
+}
+
 int blob_load(mas_context* h, const void* src, size_t size) {
     const unsigned char* in = static_cast<const unsigned char*>(src);
     MasBlobHeader hd;
@@ -151,20 +211,35 @@ int blob_load(mas_context* h, const void* src, size_t size) {
     std::vector<MasBlobSection> table(hd.nSections);
     if (hd.headerBytes + table.size() * sizeof(MasBlobSection) > size) return fail(h, MAS_ERR_ARG, "blob: table");
     std::memcpy(table.data(), in + hd.headerBytes, table.size() * sizeof(MasBlobSection));
-    // adopt the sizes, then every section must have exactly the size this handle expects
+    // The sizes every section must have, from the header alone (a scratch
+    // context: the handle is not touched until the whole blob is validated).
+    mas_context probe;
+    probe.nV = hd.nV; probe.L = hd.L; probe.totalClusters = hd.totalClusters;
+    probe.nBlk = hd.nBlk; probe.nFineBlk = hd.nFineBlk;
+    std::memcpy(probe.levelSize, hd.levelSize, sizeof(probe.levelSize));
+    if (hd.levelSize[3] > hd.totalClusters || hd.levelSize[3] < 0) return fail(h, MAS_ERR_ARG, "blob: level table");
+    const auto want = sections(&probe);
+    const MasBlobSection* sec[kSecInv + 1] = {};
+    for (auto& d : want) {
+        const MasBlobSection* t = nullptr;
+        for (auto& e : table)
+            if (e.id == d.id) t = &e;
+        if (!t || t->bytes != d.bytes || t->offset % 16 || t->offset > size || t->bytes > size - t->offset)
+            return fail(h, MAS_ERR_ARG, "blob: section");
+        sec[d.id] = t;
+    }
+    if (!blob_maps_valid(hd, in, sec)) return fail(h, MAS_ERR_ARG, "blob: index maps out of range");
+    // commit: adopt the sizes, then upload every section
     h->prepared = false;
     h->allocated = false;
     h->nV = hd.nV; h->nE = hd.nE; h->nF = hd.nF; h->L = hd.L; h->natL = hd.natL;
     h->totalClusters = hd.totalClusters; h->nBlk = hd.nBlk; h->nFineBlk = hd.nFineBlk;
     h->maxNbr = hd.maxNbr; h->nStencil = hd.nStencil;
     std::memcpy(h->levelSize, hd.levelSize, sizeof(h->levelSize));
-    auto secs = sections(h);
+    const auto secs = sections(h);
     int rc;
     for (auto& d : secs) {
-        const MasBlobSection* t = nullptr;
-        for (auto& e : table)
-            if (e.id == d.id) t = &e;
-        if (!t || t->bytes != d.bytes || t->offset + t->bytes > size) return fail(h, MAS_ERR_ARG, "blob: section");
+        const MasBlobSection* t = sec[d.id];
         if (d.buf) {
             if ((rc = ensure(h, *d.buf, d.bytes ? d.bytes : 16))) return rc;
             if (d.bytes &&

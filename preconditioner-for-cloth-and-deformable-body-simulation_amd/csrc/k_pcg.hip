@@ -213,6 +213,9 @@ __device__ __forceinline__ double dot3(float3 a, float4 b) {
 // workgroup sum of one double per thread -> partial[blockIdx.x] (fixed order)
 __device__ __forceinline__ void block_partial(double a, double* __restrict__ partial) {
     __shared__ double sa[kPcgThreads / 64];
+    // one static LDS slot array for every call in a kernel: thread 0 may still
+    // be reading the previous call's sums (k_pcg_residual calls this twice)
+    __syncthreads();
     for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
     if ((threadIdx.x & 63) == 0) sa[threadIdx.x >> 6] = a;
     __syncthreads();
@@ -466,9 +469,9 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
     PcgState init{};
     init.tol2 = (double)tol * (double)tol;
     init.maxIters = maxIters;
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
+    ScopedEvents ev;
+    if (!ev.ok()) return fail(h, MAS_ERR_HIP, "hipEventCreate");
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1];
     hipEventRecord(e0, s);
     if ((rc = hip_check(h, hipMemcpyAsync(st, &init, sizeof(init), hipMemcpyHostToDevice, s), "H2D pcg state")))
         return rc;
@@ -486,8 +489,6 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
         return rc;
     float ms = 0.f;
     hipEventElapsedTime(&ms, e0, e1);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
     if (res) {
         res->iterations = host.iters;
         res->converged = host.rr <= host.tol2 * host.bb;

@@ -44,6 +44,23 @@ struct Buffer {
     size_t bytes = 0;
 };
 
+// Timing events owned by one host call; destroyed on every return path
+// (an event recorded on a stream may be destroyed before it completes).
+struct ScopedEvents {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ScopedEvents() {
+        for (auto& x : e)
+            if (hipEventCreate(&x) != hipSuccess) x = nullptr;
+    }
+    ~ScopedEvents() {
+        for (auto& x : e)
+            if (x) hipEventDestroy(x);
+    }
+    ScopedEvents(const ScopedEvents&) = delete;
+    ScopedEvents& operator=(const ScopedEvents&) = delete;
+    bool ok() const { return e[0] && e[1]; }
+};
+
 }  // namespace mas
 
 struct mas_context {

@@ -19,9 +19,9 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
                         "copy nbrNum")))
         return rc;
     if ((rc = build_stencils(h, ef, ee, vf, efC, eeC, vfC, s))) return rc;
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
+    ScopedEvents ev;
+    if (!ev.ok()) return fail(h, MAS_ERR_HIP, "hipEventCreate");
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1];
     if ((rc = run_levels(h, s))) return rc;
     hipEventRecord(e0, s);
     if ((rc = run_assemble(h, d_diag9, d_off9, d_ranges, s))) return rc;
@@ -43,8 +43,6 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     hipEventElapsedTime(&a, h->ev[2], e0);
     hipEventElapsedTime(&b, e0, e1);
     hipEventElapsedTime(&c, e1, h->ev[3]);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
     h->stats.prepare_ms = t;
     h->stats.prepare_levels_ms = a;
     h->stats.prepare_assemble_ms = b;

@@ -143,6 +143,40 @@ def _c(a, dtype):
     return None if a is None else np.ascontiguousarray(a, dtype=dtype)
 
 
+def _host(a, dtype, count, width, name):
+    """Host array -> C-contiguous `dtype` with exactly count*width elements
+    (any shape, e.g. [n, 9] or [n, 3, 3]); raises MasError otherwise, so the
+    C ABI never copies past the caller's buffer."""
+    if a is None:
+        raise MasError(f"{name}: missing array")
+    if hasattr(a, "data_ptr"):
+        raise MasError(f"{name}: host entry point given a torch tensor (use the *Device method)")
+    arr = np.ascontiguousarray(a, dtype=dtype)
+    if arr.size != count * width:
+        raise MasError(f"{name}: expected {count} x {width} {np.dtype(dtype).name} elements, got shape {arr.shape}")
+    return arr
+
+
+def _dev(t, count, width, dtype_name, name):
+    """Device operand: a raw pointer (int, trusted) or a torch tensor that must
+    be on the GPU, C-contiguous, of the right dtype and count*width elements."""
+    if t is None:
+        raise MasError(f"{name}: missing device array")
+    if isinstance(t, int):
+        return t
+    if not hasattr(t, "data_ptr"):
+        raise MasError(f"{name}: expected a torch cuda tensor or a raw device pointer, got {type(t).__name__}")
+    if not t.is_cuda:
+        raise MasError(f"{name}: tensor is not on a GPU")
+    if str(t.dtype) != "torch." + dtype_name:
+        raise MasError(f"{name}: expected torch.{dtype_name}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise MasError(f"{name}: tensor must be contiguous")
+    if t.numel() != count * width:
+        raise MasError(f"{name}: expected {count} x {width} elements, got shape {tuple(t.shape)}")
+    return t
+
+
 class SeSchwarzPreconditioner:
     """Reference-compatible surface (SE::SeSchwarzPreconditioner) on the GPU."""
 
@@ -159,6 +193,10 @@ class SeSchwarzPreconditioner:
         self.m_faces = None       # [nF, 4] int32
         self.m_neighbours = None  # (starts, idx) CSR
         self._keep = ()
+        self._nV = 0              # set by AllocatePrecoditioner / load_blob
+        self._nnz = 0
+        self._allocated = False   # Allocate inputs present (a restored blob has none)
+        self._plans = {}
 
     def __del__(self):
         try:
@@ -168,6 +206,13 @@ class SeSchwarzPreconditioner:
         except Exception:  # interpreter shutdown
             pass
 
+    def _need(self, what, allocated=False):
+        """The C ABI's call-order error before any size check (sizes are known
+        only after Allocate / a blob load)."""
+        if not self._nV or (allocated and not self._allocated):
+            raise MasError(f"{what} failed: MAS_ERR_STATE: " +
+                           ("prepare before allocate" if allocated else "apply before prepare"))
+
     def _check(self, rc, what):
         if rc != MAS_OK:
             msg = self._L.mas_last_error(self.h)
@@ -175,23 +220,34 @@ class SeSchwarzPreconditioner:
 
     # ---- the reference's three methods ----
     def AllocatePrecoditioner(self, numVerts, numEdges, numFaces):
+        if self.m_neighbours is None:
+            raise MasError("AllocatePrecoditioner: m_neighbours (starts, idx) not set")
         starts, idx = self.m_neighbours
-        pos = _c(self.m_positions, np.float32)
-        starts = _c(starts, np.int32)
-        idx = _c(idx, np.int32)
-        edges = _c(self.m_edges, np.int32)
-        faces = _c(self.m_faces, np.int32)
+        pos = _host(self.m_positions, np.float32, numVerts, 4, "m_positions")
+        starts = _host(starts, np.int32, numVerts + 1, 1, "m_neighbours starts")
+        idx = _host(idx, np.int32, int(starts[-1]), 1, "m_neighbours idx")
+        edges = None if self.m_edges is None else _host(self.m_edges, np.int32, numEdges, 4, "m_edges")
+        faces = None if self.m_faces is None else _host(self.m_faces, np.int32, numFaces, 4, "m_faces")
         self._check(self._L.mas_allocate(self.h, numVerts, numEdges, numFaces, _ptr(pos), _ptr(starts), _ptr(idx),
                                          _ptr(edges), _ptr(faces)), "AllocatePrecoditioner")
+        self._nV, self._nnz = int(numVerts), int(starts[-1])
+        self._allocated = True
 
     AllocatePreconditioner = AllocatePrecoditioner
 
     def PreparePreconditioner(self, diagonal, csrOffDiagonals, csrRanges, efSets=None, eeSets=None, vfSets=None,
                               efCounts=None, eeCounts=None, vfCounts=None):
-        d = _c(diagonal, np.float32)
-        o = _c(csrOffDiagonals, np.float32)
-        r = _c(csrRanges, np.int32)
+        self._need("PreparePreconditioner", allocated=True)
+        nV, nnz = self._nV, self._nnz
+        d = _host(diagonal, np.float32, nV, 9, "diagonal")
+        o = _host(csrOffDiagonals, np.float32, nnz, 9, "csrOffDiagonals")
+        r = _host(csrRanges, np.int32, nV + 1, 1, "csrRanges")
         efC, eeC, vfC = (_c(x, np.uint32) for x in (efCounts, eeCounts, vfCounts))
+        for sets, cnt, name in ((efSets, efC, "ef"), (eeSets, eeC, "ee"), (vfSets, vfC, "vf")):
+            n = int(cnt[-1]) if cnt is not None and cnt.size else 0
+            if n and (sets is None or np.asarray(sets).nbytes < 48 * n):
+                raise MasError(f"{name}Sets: {n} records of 48 B expected")
+        self._plans = {}
         self._check(self._L.mas_prepare(self.h, _ptr(d), _ptr(o), _ptr(r), _ptr(efSets), _ptr(eeSets), _ptr(vfSets),
                                         _ptr(efC), _ptr(eeC), _ptr(vfC)), "PreparePreconditioner")
 
@@ -201,40 +257,70 @@ class SeSchwarzPreconditioner:
         tensors (e.g. a GPU collision pass's output buffers)."""
         efC, eeC, vfC = (x if (x is None or hasattr(x, "data_ptr") or isinstance(x, int)) else _c(x, np.uint32)
                          for x in (efCounts, eeCounts, vfCounts))
+        self._need("PreparePreconditionerDevice", allocated=True)
+        d_diag = _dev(d_diag, self._nV, 9, "float32", "d_diag")
+        d_off = _dev(d_off, self._nnz, 9, "float32", "d_off")
+        d_ranges = _dev(d_ranges, self._nV + 1, 1, "int32", "d_ranges")
+        self._plans = {}
         self._check(self._L.mas_prepare_device(self.h, _ptr(d_diag), _ptr(d_off), _ptr(d_ranges), _ptr(efSets),
                                                _ptr(eeSets), _ptr(vfSets), _ptr(efC), _ptr(eeC), _ptr(vfC),
                                                _ptr(stream)), "PreparePreconditionerDevice")
 
     def Preconditioning(self, z, residual, dim=None):
-        r = _c(residual, np.float32)
-        out = np.empty_like(r) if z is None else z
+        self._need("Preconditioning")
+        nV = self._nV
+        r = _host(residual, np.float32, nV, 4, "residual")
+        if z is None:
+            out = np.empty((nV, 4), np.float32)
+        else:  # written in place: must be exactly the C layout
+            if not (isinstance(z, np.ndarray) and z.dtype == np.float32 and z.flags.c_contiguous
+                    and z.flags.writeable and z.size == nV * 4):
+                raise MasError("Preconditioning: z must be a writable C-contiguous float32 array of nV x 4")
+            out = z
         self._check(self._L.mas_apply(self.h, _ptr(out), _ptr(r)), "Preconditioning")
         return out
 
     def PreconditioningDevice(self, z, residual, stream=None):
         """z, residual: torch cuda float32 tensors [nV, 4] (or raw device pointers)."""
+        self._need("PreconditioningDevice")
+        z = _dev(z, self._nV, 4, "float32", "z")
+        residual = _dev(residual, self._nV, 4, "float32", "residual")
         self._check(self._L.mas_apply_device(self.h, _ptr(z), _ptr(residual), _ptr(stream)), "PreconditioningDevice")
 
     # ---- Morton-range sharding (include/mas_capi.h) ----
     def shard_setup(self, rank, world) -> dict:
         sh = mas_shard()
         self._check(self._L.mas_shard_setup(self.h, rank, world, ctypes.byref(sh)), "shard_setup")
-        return sh.as_dict()
+        self._plans[(rank, world)] = sh.as_dict()  # valid until the next Prepare / blob load
+        return dict(self._plans[(rank, world)])
+
+    def _shard_vecs(self, rank, world, **kw):
+        plan = self._plans.get((rank, world)) or self.shard_setup(rank, world)
+        sizes = {"r": self._nV, "z": self._nV, "seg": plan["seg_max"], "gathered": world * plan["seg_max"]}
+        return {k: _dev(v, sizes[k], 4, "float32", k) for k, v in kw.items()}
 
     def shard_restrict(self, rank, world, r, seg, stream=None):
+        v = self._shard_vecs(rank, world, r=r, seg=seg)
+        r, seg = v["r"], v["seg"]
         self._check(self._L.mas_apply_shard_restrict(self.h, rank, world, _ptr(r), _ptr(seg), _ptr(stream)),
                     "shard_restrict")
 
     def shard_finish(self, rank, world, gathered, r, z, stream=None):
+        v = self._shard_vecs(rank, world, gathered=gathered, r=r, z=z)
+        gathered, r, z = v["gathered"], v["r"], v["z"]
         self._check(self._L.mas_apply_shard_finish(self.h, rank, world, _ptr(gathered), _ptr(r), _ptr(z),
                                                    _ptr(stream)), "shard_finish")
 
     def shard_fine(self, rank, world, r, z, stream=None):
         """Overlapped step 3a: own level-0 blocks, z = Z0 (no coarse terms)."""
+        v = self._shard_vecs(rank, world, r=r, z=z)
+        r, z = v["r"], v["z"]
         self._check(self._L.mas_apply_shard_fine(self.h, rank, world, _ptr(r), _ptr(z), _ptr(stream)), "shard_fine")
 
     def shard_complete(self, rank, world, gathered, z, stream=None):
         """Overlapped step 3b: coarse levels from the gathered segments, z += prolongation."""
+        v = self._shard_vecs(rank, world, gathered=gathered, z=z)
+        gathered, z = v["gathered"], v["z"]
         self._check(self._L.mas_apply_shard_complete(self.h, rank, world, _ptr(gathered), _ptr(z), _ptr(stream)),
                     "shard_complete")
 
@@ -242,11 +328,13 @@ class SeSchwarzPreconditioner:
     def pcg_solve(self, diagonal, csrOffDiagonals, csrRanges, b, x0=None, max_iters=1000, tol=1e-5,
                   precondition=True):
         """Host arrays: returns (x [nV,4] float32, result dict)."""
-        d = _c(diagonal, np.float32)
-        o = _c(csrOffDiagonals, np.float32)
-        r = _c(csrRanges, np.int32)
-        bb = _c(b, np.float32)
-        x = np.zeros_like(bb) if x0 is None else np.array(x0, dtype=np.float32, copy=True)
+        self._need("pcg_solve", allocated=True)
+        nV, nnz = self._nV, self._nnz
+        d = _host(diagonal, np.float32, nV, 9, "diagonal")
+        o = _host(csrOffDiagonals, np.float32, nnz, 9, "csrOffDiagonals")
+        r = _host(csrRanges, np.int32, nV + 1, 1, "csrRanges")
+        bb = _host(b, np.float32, nV, 4, "b")
+        x = np.zeros_like(bb) if x0 is None else np.array(_host(x0, np.float32, nV, 4, "x0"), copy=True)
         res = mas_pcg_result()
         self._check(self._L.mas_pcg_solve(self.h, _ptr(d), _ptr(o), _ptr(r), _ptr(x), _ptr(bb), int(max_iters),
                                           float(tol), int(bool(precondition)), ctypes.byref(res)), "pcg_solve")
@@ -255,6 +343,13 @@ class SeSchwarzPreconditioner:
     def pcg_solve_device(self, d_diag, d_off, d_ranges, x, b, max_iters=1000, tol=1e-5, precondition=True,
                          stream=None) -> dict:
         """Device arrays (torch cuda tensors or raw pointers); x is updated in place."""
+        self._need("pcg_solve_device", allocated=True)
+        nV = self._nV
+        d_diag = _dev(d_diag, nV, 9, "float32", "d_diag")
+        d_off = _dev(d_off, self._nnz, 9, "float32", "d_off")
+        d_ranges = _dev(d_ranges, nV + 1, 1, "int32", "d_ranges")
+        x = _dev(x, nV, 4, "float32", "x")
+        b = _dev(b, nV, 4, "float32", "b")
         res = mas_pcg_result()
         self._check(self._L.mas_pcg_solve_device(self.h, _ptr(d_diag), _ptr(d_off), _ptr(d_ranges), _ptr(x),
                                                  _ptr(b), int(max_iters), float(tol), int(bool(precondition)),
@@ -274,7 +369,10 @@ class SeSchwarzPreconditioner:
     def load_blob(self, blob):
         b = np.ascontiguousarray(np.frombuffer(blob, dtype=np.uint8) if isinstance(blob, (bytes, bytearray))
                                  else blob, dtype=np.uint8)
+        self._plans = {}
         self._check(self._L.mas_load_blob(self.h, _ptr(b), b.nbytes), "load_blob")
+        self._nV, self._nnz = self.info()["num_verts"], 0  # a restored handle applies; Prepare needs Allocate
+        self._allocated = False
 
     # ---- introspection ----
     def set_profiling(self, on: bool):

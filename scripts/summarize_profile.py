@@ -3,6 +3,7 @@ profiles/<round>/ (kernel stats CSV + PMC per-kernel means + markdown)."""
 import collections, csv, json, os, shutil, sys
 
 src, dst = sys.argv[1], sys.argv[2]
+commit = sys.argv[3] if len(sys.argv) > 3 else None  # the commit the profiled tree was at
 os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
 for f in ("bench.json", "bench_trace.json", "smoke.log", "pytest_gpu.log"):
@@ -29,7 +30,8 @@ for name, r in stats.items():
 lines += ["", "## HBM traffic per launch (separate --pmc passes; FETCH_SIZE x 2 per the gfx950 wide-read "
           "correction, WRITE_SIZE as reported; KB = 1024 B)", "",
           "| kernel | FETCH_SIZE KB | WRITE_SIZE KB | corrected bytes (2*FETCH + WRITE) |", "|---|---|---|---|"]
-out = {}
+out = {"__meta__": {"commit": commit, "workload": bench["config"]["workload"],
+                    "passes": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE (separate runs)"}}
 for name in sorted({k[0] for k in pmc}):
     f = pmc.get((name, "FETCH_SIZE"), [0]); w = pmc.get((name, "WRITE_SIZE"), [0])
     if len(f) < 3:

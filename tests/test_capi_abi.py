@@ -69,3 +69,23 @@ def test_null_handle_and_bad_args():
     assert L.mas_destroy(None) == -1
     assert L.mas_apply(None, None, None) == -1
     assert L.mas_create(None, None) == -1
+
+
+def test_wrapper_operand_checks_without_gpu():
+    """The binding refuses wrongly shaped / typed operands before any copy
+    (the C ABI copies exactly nV*16, nnz*36, (nV+1)*4 bytes)."""
+    import numpy as np
+    import torch
+    import mas_amd
+    from mas_amd import _host, _dev, MasError
+    ok = _host(np.zeros((5, 3, 3), np.float64), np.float32, 5, 9, "diag")
+    assert ok.dtype == np.float32 and ok.flags.c_contiguous and ok.size == 45
+    with pytest.raises(MasError, match="expected 5 x 4"):
+        _host(np.zeros((5, 3), np.float32), np.float32, 5, 4, "r")
+    with pytest.raises(MasError, match="torch tensor"):
+        _host(torch.zeros(5, 4), np.float32, 5, 4, "r")
+    assert _dev(1234, 5, 4, "float32", "z") == 1234  # raw pointers are the caller's contract
+    with pytest.raises(MasError, match="not on a GPU"):
+        _dev(torch.zeros(5, 4), 5, 4, "float32", "z")
+    with pytest.raises(MasError, match="torch cuda tensor"):
+        _dev(np.zeros((5, 4), np.float32), 5, 4, "float32", "z")

@@ -90,3 +90,61 @@ def test_golden_blob_reproduced():
     blob = _prepared(cloth(12)).save_blob()
     assert blob.nbytes == golden.nbytes
     np.testing.assert_array_equal(blob, golden)
+
+
+def _fnv1a(buf):
+    h = 1469598103934665603
+    for b in buf.tobytes():
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_blob_rejects_out_of_range_maps():
+    """A blob whose checksum is valid but whose index maps point outside the
+    level table (a crafted file: FNV-1a is no tamper check) is refused before
+    the handle is touched."""
+    import mas_amd
+    mesh = cloth(16)
+    P = _prepared(mesh)
+    blob = P.save_blob()
+    header_bytes = int(blob[12:16].view(np.uint32)[0])
+    n_sec = int(blob[128:132].view(np.int32)[0])
+    table = blob[header_bytes:header_bytes + 24 * n_sec].reshape(n_sec, 24)
+    sec = {int(t[:4].view(np.uint32)[0]): (int(t[8:16].view(np.uint64)[0]), int(t[16:24].view(np.uint64)[0]))
+           for t in table}
+    Q = mas_amd.SeSchwarzPreconditioner()
+    Q.load_blob(blob)
+    for sid, word in ((8, 1), (2, 5), (5, 3)):  # vmap ancestor, s2o, goingNext
+        bad = blob.copy()
+        nbytes, off = sec[sid]
+        bad[off + 4 * word: off + 4 * word + 4] = np.array([1 << 28], np.int32).view(np.uint8)
+        bad[144:152] = np.array([_fnv1a(bad[header_bytes:])], np.uint64).view(np.uint8)
+        with pytest.raises(mas_amd.MasError, match="out of range"):
+            Q.load_blob(bad)
+        # the handle still holds the last good blob and applies
+        r = np.ones((mesh.nV, 4), np.float32)
+        np.testing.assert_array_equal(Q.Preconditioning(None, r), P.Preconditioning(None, r))
+
+
+def test_wrappers_reject_bad_operands():
+    """Shape / dtype / layout checks before the C ABI copies nV*16 bytes."""
+    import torch
+    import mas_amd
+    mesh = cloth(16)
+    P = _prepared(mesh)
+    n = mesh.nV
+    with pytest.raises(mas_amd.MasError, match="residual"):
+        P.Preconditioning(None, np.zeros((n, 3), np.float32))
+    with pytest.raises(mas_amd.MasError, match="z must be"):
+        P.Preconditioning(np.zeros((n, 4), np.float64), np.zeros((n, 4), np.float32))
+    with pytest.raises(mas_amd.MasError, match="csrOffDiagonals"):
+        P.PreparePreconditioner(mesh.diag, mesh.off[:-1], mesh.starts)
+    r = torch.zeros((n, 4), device="cuda")
+    with pytest.raises(mas_amd.MasError, match="contiguous"):
+        P.PreconditioningDevice(torch.zeros((4, n), device="cuda").t(), r)
+    with pytest.raises(mas_amd.MasError, match="float32"):
+        P.PreconditioningDevice(torch.zeros((n, 4), device="cuda", dtype=torch.float64), r)
+    with pytest.raises(mas_amd.MasError, match="not on a GPU"):
+        P.PreconditioningDevice(torch.zeros((n, 4)), r)
+    with pytest.raises(mas_amd.MasError, match="elements"):
+        P.PreconditioningDevice(torch.zeros((n - 1, 4), device="cuda"), r)

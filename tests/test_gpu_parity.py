@@ -113,6 +113,30 @@ def test_device_path_and_determinism():
     np.testing.assert_array_equal(z1, z_host)                 # host and device entry points agree
 
 
+def test_256k_cloth_parity():
+    """BASELINE configs[1]: the 512^2 grid at 3 levels (natural 4).  Maps
+    bit-exact, level sizes and the active block count of the survey probe
+    (262 144 / 8 192 / 256 nodes, 8 456 blocks), contact-free coarse blocks
+    bit-exact, z within 1e-5 of the oracle."""
+    from mas_amd import meshgen
+    mesh, cfg = meshgen.build_config("256k")
+    assert mesh.nV == 262144 and cfg["levels"] == 3
+    P = _gpu(mesh, cfg["levels"])
+    o = _oracle(mesh, cfg["levels"], threads=8)
+    compare_maps(P, o, mesh.nV)
+    inf = P.info()
+    assert [int(n) for n in inf["level_size"][:3, 0]] == [262144, 8192, 256]
+    assert inf["num_blocks"] == 8456 and inf["total_clusters"] == o.total_clusters == 8456 * 32
+    nfine = (mesh.nV + 31) // 32
+    for blk in list(range(nfine, inf["num_blocks"], 37)) + [inf["num_blocks"] - 1]:
+        np.testing.assert_array_equal(P.block_matrix(blk), o.block_matrix(blk))
+    for blk in (0, nfine // 3, nfine - 1):
+        np.testing.assert_array_equal(P.block_inverse(blk), o.block_inverse(blk))
+    for seed in (0x5EED + 1, 11):
+        r = meshgen.residual(mesh.nV, seed)
+        assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
+
+
 def test_1m_cloth_parity():
     from mas_amd import meshgen
     mesh = cloth(1024)

@@ -35,7 +35,11 @@ def _true_rel_res(mesh, x, b):
     return float(np.linalg.norm(bv - A @ xv) / np.linalg.norm(bv))
 
 
-@pytest.mark.parametrize("W,L,band", [(100, 3, (0.15, 0.30)), (100, 1, (0.35, 0.60))])
+# SURVEY §4 known answers (reference probe, fp64 PCG, tol 1e-5): 100^2 / L3
+# 526 -> 110 (0.21), 100^2 / L1 526 -> 232 (0.44), 256^2 / L4 515 -> 93
+# (0.18).  The probe's right-hand side was not recorded, so the ratio is held
+# to a band around it.
+@pytest.mark.parametrize("W,L,band", [(100, 3, (0.15, 0.30)), (100, 1, (0.35, 0.60)), (256, 4, (0.13, 0.25))])
 def test_pcg_iterations_match_cpu_and_known_answer(W, L, band):
     from mas_amd import meshgen
     from oracle import Oracle

@@ -36,14 +36,18 @@ def _virtual_sharded(P, r, world, overlap=False):
     return z
 
 
-@pytest.mark.parametrize("kind,W,L,worlds", [("cloth", 64, 0, (1, 2, 3, 8)), ("cloth", 100, 1, (2, 5)),
-                                             ("tet", 16, 3, (2, 4)), ("cloth", 1024, 4, (2, 8))])
-def test_virtual_shards_bitwise(kind, W, L, worlds):
+@pytest.mark.parametrize("kind,W,L,worlds,nc", [("cloth", 64, 0, (1, 2, 3, 8), 0), ("cloth", 100, 1, (2, 5), 0),
+                                                ("tet", 16, 3, (2, 4), 0), ("cloth", 1024, 4, (2, 8), 0),
+                                                ("cloth", 1024, 4, (8,), 100_000), ("tet", 160, 4, (8,), 0)])
+def test_virtual_shards_bitwise(kind, W, L, worlds, nc):
+    """Includes BASELINE configs[3] (1M + 100k VF contacts, 8 ranks) and
+    configs[4] (4M tet lattice, 8 ranks: ~26k level-1 nodes per rank)."""
     import torch
     import mas_amd
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
-    P = mas_amd.from_mesh(mesh, max_levels=L)
+    contacts = meshgen.vf_contacts(mesh, nc, seed=3) if nc else None
+    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
     r = torch.from_numpy(meshgen.residual(mesh.nV, 3)).cuda()
     z_ref = torch.zeros_like(r)
     torch.cuda.synchronize()
