@@ -205,6 +205,11 @@ int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_g
 int mas_blob_size(mas_handle h, size_t* out_bytes);
 int mas_save_blob(mas_handle h, void* dst, size_t capacity, size_t* written);
 int mas_load_blob(mas_handle h, const void* src, size_t size);
+/* Checks a blob without a device or handle: header, checksum, section sizes
+ * and that every index map stays inside the level table (FNV-1a detects
+ * corruption, not tampering; mas_load_blob runs the same checks first).
+ * MAS_OK or MAS_ERR_ARG. */
+int mas_blob_validate(const void* src, size_t size);
 /* introspection / parity */
 int mas_get_info(mas_handle h, mas_info* out);
 int mas_get_stats(mas_handle h, mas_stats* out);

@@ -139,13 +139,16 @@ int blob_save(mas_context* h, void* dst, size_t cap, size_t* written) {
 static bool blob_maps_valid(const MasBlobHeader& hd, const unsigned char* in, const MasBlobSection* sec[]) {
     const int nV = hd.nV, L = hd.L, tc = hd.totalClusters;
     const int* ls = hd.levelSize;
-    // level table: level 0 = (nV, 0), begin_{l+1} = begin_l + ceil32(n_l), total = begin_L
-    if (ls[0] != nV || ls[1] != 0) return false;
-    for (int l = 0; l < L; ++l) {
+    // level table: entry l >= 1 = (n_l, begin_l), begin_1 = ceil32(nV),
+    // begin_{l+1} = begin_l + ceil32(n_l), total = begin_L (entry 0 is unused)
+    if (ls[3] != (nV + 31) / 32 * 32) return false;
+    for (int l = 1; l < L; ++l) {
         const long long n = ls[2 * l], b = ls[2 * l + 1];
-        if (n < 0 || (l > 0 && n > ls[2 * (l - 1)]) || b + (n + 31) / 32 * 32 != ls[2 * (l + 1) + 1]) return false;
+        if (n <= 0 || n > (l == 1 ? nV : ls[2 * (l - 1)]) || b + (n + 31) / 32 * 32 != ls[2 * (l + 1) + 1])
+            return false;
     }
     if (ls[2 * L + 1] != tc) return false;
+    auto count = [&](int l) { return l == 0 ? nV : ls[2 * l]; };
     auto arr = [&](int i) { return reinterpret_cast<const int*>(in + sec[i]->offset); };
     std::vector<int> seen((size_t)nV, 0);
     const int* s2o = arr(kSecS2o);
@@ -154,13 +157,13 @@ static bool blob_maps_valid(const MasBlobHeader& hd, const unsigned char* in, co
         if (s2o[v] < 0 || s2o[v] >= nV || seen[s2o[v]]++ || o2s[s2o[v]] != v) return false;
     }
     const int* gn = arr(kSecGoingNext);
-    for (int i = 0; i < tc; ++i)
-        if (gn[i] < 0 || gn[i] >= tc) return false;
+    for (int i = 0; i < tc; ++i)  // the top level points at the sentinel total (.cpp:1244)
+        if (gn[i] < 0 || gn[i] > tc) return false;
     const int* cst = arr(kSecCst);
     for (int l = 0; l < L; ++l)
         for (int v = 0; v < nV; ++v) {
             const int c = cst[(size_t)l * nV + v];
-            if (c < 0 || (l + 1 < L && c >= ls[2 * (l + 1)])) return false;
+            if (c < 0 || (l + 1 < L && c >= count(l + 1))) return false;
         }
     const int* ct = arr(kSecCoarseTables);
     for (size_t i = 0; i < (size_t)nV * 4; ++i)
@@ -172,63 +175,70 @@ static bool blob_maps_valid(const MasBlobHeader& hd, const unsigned char* in, co
         const int a[4] = {vm[v].x, vm[v].y, vm[v].z, vm[v].w};
         if (a[0] != s2o[v]) return false;
         for (int l = 1; l < np; ++l)
-            if (a[l] < ls[2 * l + 1] || a[l] >= ls[2 * l + 1] + ls[2 * l]) return false;
+            if (a[l] < ls[2 * l + 1] || a[l] >= ls[2 * l + 1] + count(l)) return false;
     }
     // coarse members (child bank, component mask): inside the child level
     const int begin1 = ls[3];
     const int2* mb = reinterpret_cast<const int2*>(in + sec[kSecMembers]->offset);
     for (int l = 1; l < L; ++l) {
-        const int nChild = ls[2 * (l - 1)];
-        for (int p = 0; p < (ls[2 * l] + 31) / 32 * 32; ++p) {
+        const int nChild = count(l - 1);
+        for (int p = 0; p < (count(l) + 31) / 32 * 32; ++p) {
             const int2 m = mb[ls[2 * l + 1] + p - begin1];
             if (m.x < 0 || (m.y != 0 && 32LL * m.x + 32 - __builtin_clz((unsigned)m.y) > nChild)) return false;
-            if (p >= ls[2 * l] && m.y != 0) return false;  // padding nodes have no children
+            if (p >= count(l) && m.y != 0) return false;  // padding nodes have no children
         }
     }
     // level-1 segment starts per level-0 bank: 0 .. n1, nondecreasing
     const int* f = arr(kSecL1First);
-    const int n1 = L > 1 ? ls[2] : 0;
+    const int n1 = L > 1 ? count(1) : 0;
     for (int b = 0; b <= hd.nFineBlk; ++b)
         if (f[b] < 0 || f[b] > n1 || (b > 0 && f[b] < f[b - 1])) return false;
     return f[hd.nFineBlk] == n1;
 }
 
-int blob_load(mas_context* h, const void* src, size_t size) {
-    const unsigned char* in = static_cast<const unsigned char*>(src);
-    MasBlobHeader hd;
-    if (!src || size < sizeof(hd)) return fail(h, MAS_ERR_ARG, "blob: too short");
+// Header, checksum, section table and index maps; no device work, nothing
+// of a handle is touched.  On success sec[id] points at each section entry.
+static int blob_parse(const unsigned char* in, size_t size, MasBlobHeader& hd, const MasBlobSection* sec[],
+                      std::vector<MasBlobSection>& table, std::string& why) {
+    auto bad = [&](const char* m) { why = m; return MAS_ERR_ARG; };
+    if (!in || size < sizeof(hd)) return bad("blob: too short");
     std::memcpy(&hd, in, sizeof(hd));
-    if (std::memcmp(hd.magic, kBlobMagic, 8) != 0) return fail(h, MAS_ERR_ARG, "blob: bad magic");
-    if (hd.version != kBlobVersion) return fail(h, MAS_ERR_ARG, "blob: unsupported version");
+    if (std::memcmp(hd.magic, kBlobMagic, 8) != 0) return bad("blob: bad magic");
+    if (hd.version != kBlobVersion) return bad("blob: unsupported version");
     if (hd.headerBytes < sizeof(hd) || hd.headerBytes > size || hd.nSections <= 0 || hd.nSections > 64 ||
         hd.headerBytes + hd.payloadBytes != size)
-        return fail(h, MAS_ERR_ARG, "blob: inconsistent sizes");
-    if (fnv1a(in + hd.headerBytes, size - hd.headerBytes) != hd.checksum)
-        return fail(h, MAS_ERR_ARG, "blob: checksum mismatch");
+        return bad("blob: inconsistent sizes");
+    if (fnv1a(in + hd.headerBytes, size - hd.headerBytes) != hd.checksum) return bad("blob: checksum mismatch");
     if (hd.nV <= 0 || hd.L < 1 || hd.L > kMaxLevels || hd.nBlk <= 0 || hd.nFineBlk != (hd.nV + 31) / 32 ||
-        hd.totalClusters != 32 * hd.nBlk)
-        return fail(h, MAS_ERR_ARG, "blob: inconsistent header");
-    std::vector<MasBlobSection> table(hd.nSections);
-    if (hd.headerBytes + table.size() * sizeof(MasBlobSection) > size) return fail(h, MAS_ERR_ARG, "blob: table");
+        hd.totalClusters != 32 * hd.nBlk || hd.levelSize[3] < 0 || hd.levelSize[3] > hd.totalClusters)
+        return bad("blob: inconsistent header");
+    table.resize(hd.nSections);
+    if (hd.headerBytes + table.size() * sizeof(MasBlobSection) > size) return bad("blob: table");
     std::memcpy(table.data(), in + hd.headerBytes, table.size() * sizeof(MasBlobSection));
-    // The sizes every section must have, from the header alone (a scratch
-    // context: the handle is not touched until the whole blob is validated).
+    // the sizes every section must have, from the header alone (a scratch context)
     mas_context probe;
     probe.nV = hd.nV; probe.L = hd.L; probe.totalClusters = hd.totalClusters;
     probe.nBlk = hd.nBlk; probe.nFineBlk = hd.nFineBlk;
     std::memcpy(probe.levelSize, hd.levelSize, sizeof(probe.levelSize));
-    if (hd.levelSize[3] > hd.totalClusters || hd.levelSize[3] < 0) return fail(h, MAS_ERR_ARG, "blob: level table");
-    const auto want = sections(&probe);
-    const MasBlobSection* sec[kSecInv + 1] = {};
-    for (auto& d : want) {
+    for (auto& d : sections(&probe)) {
         const MasBlobSection* t = nullptr;
         for (auto& e : table)
             if (e.id == d.id) t = &e;
         if (!t || t->bytes != d.bytes || t->offset % 16 || t->offset > size || t->bytes > size - t->offset)
-            return fail(h, MAS_ERR_ARG, "blob: section");
+            return bad("blob: section");
         sec[d.id] = t;
     }
-    if (!blob_maps_valid(hd, in, sec)) return fail(h, MAS_ERR_ARG, "blob: index maps out of range");
+    if (!blob_maps_valid(hd, in, sec)) return bad("blob: index maps out of range");
+    return MAS_OK;
+}
+
+int blob_load(mas_context* h, const void* src, size_t size) {
+    const unsigned char* in = static_cast<const unsigned char*>(src);
+    MasBlobHeader hd;
+    const MasBlobSection* sec[kSecInv + 1] = {};
+    std::vector<MasBlobSection> table;
+    std::string why;
+    if (blob_parse(in, size, hd, sec, table, why) != MAS_OK) return fail(h, MAS_ERR_ARG, why);
     // commit: adopt the sizes, then upload every section
     h->prepared = false;
     h->allocated = false;
@@ -281,6 +291,14 @@ int mas_save_blob(mas_handle h, void* dst, size_t capacity, size_t* written) {
     if (h->prepared && h->l1First.empty())  // computed lazily after Prepare (k_shard.hip)
         if (int rc = compute_l1_first(h, h->stream)) return rc;
     return blob_save(h, dst, capacity, written);
+}
+
+int mas_blob_validate(const void* src, size_t size) {
+    MasBlobHeader hd;
+    const MasBlobSection* sec[kSecInv + 1] = {};
+    std::vector<MasBlobSection> table;
+    std::string why;
+    return blob_parse(static_cast<const unsigned char*>(src), size, hd, sec, table, why);
 }
 
 int mas_load_blob(mas_handle h, const void* src, size_t size) {

@@ -34,7 +34,8 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
            "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
            "mas_apply_shard_fine", "mas_apply_shard_complete",
-           "mas_pcg_solve_device", "mas_pcg_solve", "mas_blob_size", "mas_save_blob", "mas_load_blob"]
+           "mas_pcg_solve_device", "mas_pcg_solve", "mas_blob_size", "mas_save_blob", "mas_load_blob",
+           "mas_blob_validate"]
 
 
 class mas_config(ctypes.Structure):
@@ -125,6 +126,7 @@ def lib():
         L.mas_blob_size.argtypes = [P, ctypes.POINTER(ctypes.c_size_t)]
         L.mas_save_blob.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.mas_load_blob.argtypes = [P, P, ctypes.c_size_t]
+        L.mas_blob_validate.argtypes = [P, ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -432,6 +434,13 @@ def from_mesh(mesh, max_levels=0, contacts=None, **kw) -> SeSchwarzPreconditione
         vf, vfC = contacts
         P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, vf, None, None, vfC)
     return P
+
+
+def blob_validate(blob) -> int:
+    """mas_blob_validate: MAS_OK (0) or MAS_ERR_ARG; needs no device."""
+    b = np.ascontiguousarray(np.frombuffer(blob, dtype=np.uint8) if isinstance(blob, (bytes, bytearray))
+                             else blob, dtype=np.uint8)
+    return lib().mas_blob_validate(_ptr(b), b.nbytes)
 
 
 def shard_plan(nV, l1_first, rank, world) -> dict:

@@ -101,3 +101,32 @@ def test_golden_blob_matches_oracle():
         for s, (i, j) in enumerate(ij):
             got[i, j] = got[j, i] = inv[blk, s]
         np.testing.assert_array_equal(got, ref)  # GPU inverses bit-exact with the oracle's
+
+
+def _fnv1a(buf):
+    h = 1469598103934665603
+    for b in buf.tobytes():
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_blob_validate_without_device():
+    """mas_blob_validate (no GPU): the golden blob passes; a blob whose
+    checksum is valid but whose maps leave the level table is refused."""
+    import mas_amd
+    blob = np.fromfile(BLOB, dtype=np.uint8)
+    assert mas_amd.blob_validate(blob) == 0
+    hb = int(blob[12:16].view(np.uint32)[0])
+    ns = int(blob[128:132].view(np.int32)[0])
+    tab = blob[hb:hb + 24 * ns].reshape(ns, 24)
+    sec = {int(t[:4].view(np.uint32)[0]): (int(t[8:16].view(np.uint64)[0]), int(t[16:24].view(np.uint64)[0]))
+           for t in tab}
+    for sid, word, val in ((8, 1, 1 << 28), (2, 5, -3), (5, 3, 1 << 20), (9, 0, 1 << 20), (10, 2, -1)):
+        bad = blob.copy()
+        off = sec[sid][1]
+        bad[off + 4 * word: off + 4 * word + 4] = np.array([val], np.int32).view(np.uint8)
+        bad[144:152] = np.array([_fnv1a(bad[hb:])], np.uint64).view(np.uint8)
+        assert mas_amd.blob_validate(bad) == -1, sid
+    bad = blob.copy()
+    bad[-1] ^= 1
+    assert mas_amd.blob_validate(bad) == -1  # checksum
