@@ -50,7 +50,8 @@ typedef enum {
     MAS_ERR_STATE = -4,    /* call order violated (prepare before allocate, ...)  */
     MAS_ERR_LEVELS = -5,   /* more than 5 levels requested (reference B-6)        */
     MAS_ERR_NOMEM = -6,    /* device allocation failed                           */
-    MAS_ERR_NO_DEVICE = -7 /* no HIP device / kernels not loadable                */
+    MAS_ERR_NO_DEVICE = -7, /* no HIP device / kernels not loadable               */
+    MAS_ERR_COMM = -8       /* the allgather hook / RCCL failed (see mas_last_error) */
 } mas_status;
 
 typedef struct mas_context* mas_handle;
@@ -192,6 +193,37 @@ int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gat
 int mas_apply_shard_fine(mas_handle h, int rank, int world, const float* d_r4, float* d_z4, void* stream);
 int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_gathered4, float* d_z4,
                              void* stream);
+
+/* ---- one-call sharded apply with the collective inside the library ----
+ * The whole per-rank Preconditioning of a Morton-range shard behind the
+ * reference's apply (SeSchwarzPreconditioner.h:63), so a C/C++ simulator that
+ * links the library can shard without Python: restrict the own level-1
+ * segment, allgather the segments, solve.  The level-0 block solves of the
+ * rank run on `stream` while the allgather is in flight on the handle's own
+ * communication stream (which first waits for the restrict); the coarse
+ * levels and the prolongation follow once it is done.
+ * z is written for the rank's own vertices only; the union over ranks is
+ * bitwise equal to mas_apply_device.  The segment buffers belong to the
+ * handle.
+ *
+ * mas_allgather_fn: enqueue on `stream` (a hipStream_t) an allgather of
+ * `bytes` from `send` into `recv` (world x bytes, rank-major) and return 0, or
+ * nonzero on failure (reported as MAS_ERR_COMM).  It is called from the
+ * calling thread during mas_shard_apply_device; `user` is passed through.
+ * allgather may be NULL only when world == 1. */
+typedef int (*mas_allgather_fn)(const void* send, void* recv, size_t bytes, void* stream, void* user);
+int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn allgather, void* user, float* d_z4,
+                           const float* d_r4, void* stream);
+
+/* The same over RCCL (xGMI) with a communicator the handle owns.  RCCL is
+ * loaded at run time (librccl.so.1; the one already in the process if any).
+ * mas_rccl_unique_id: rank 0 creates the 128-byte id and the caller
+ * broadcasts it (any out-of-band channel); every rank then calls
+ * mas_rccl_init with it on its own device.  mas_shard_apply_rccl uses the
+ * communicator's rank and size. */
+int mas_rccl_unique_id(void* id128);
+int mas_rccl_init(mas_handle h, const void* id128, int rank, int world);
+int mas_shard_apply_rccl(mas_handle h, float* d_z4, const float* d_r4, void* stream);
 
 /* ---- fixture / wire format ----
  * A prepared handle as one versioned, checksummed blob (header "MASBLOB",

@@ -17,6 +17,7 @@
 // Every value is computed by the same kernel arithmetic as the unsharded
 // apply, so the union of the ranks' outputs is bitwise equal to it.
 #include <algorithm>
+#include <string>
 #include <vector>
 
 #include "block_solve.h"
@@ -309,6 +310,52 @@ int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_g
     h->shardPendingEv = nullptr;
     h->stats.apply_calls++;
     return hip_check(h, hipGetLastError(), "shard complete");
+}
+
+// The whole per-rank apply with the collective inside (include/mas_capi.h):
+// restrict on `stream`, the allgather hook on the handle's communication
+// stream (which waits for the restrict), the own level-0 blocks on `stream`
+// meanwhile, then `stream` waits for the gather and runs the coarse levels and
+// the prolongation.  One rank has nothing to hide: the serial form.
+int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn allgather, void* user, float* d_z4,
+                           const float* d_r4, void* stream) {
+    if (!h) return MAS_ERR_ARG;
+    if (!d_z4 || !d_r4) return fail(h, MAS_ERR_ARG, "mas_shard_apply_device: null vector");
+    if ((reinterpret_cast<uintptr_t>(d_z4) | reinterpret_cast<uintptr_t>(d_r4)) & 15)
+        return fail(h, MAS_ERR_ARG, "mas_shard_apply_device: vectors must be 16-byte aligned");
+    if (!allgather && world != 1) return fail(h, MAS_ERR_ARG, "mas_shard_apply_device: no allgather for world > 1");
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    hipSetDevice(h->device);
+    mas_shard sh;
+    int rc = mas_shard_setup(h, rank, world, &sh);
+    if (rc) return rc;
+    const size_t segBytes = (size_t)sh.seg_max * 16;
+    if ((rc = ensure(h, h->shardSeg, segBytes)) || (rc = ensure(h, h->shardGathered, segBytes * world))) return rc;
+    if (!h->commStream) {
+        if ((rc = hip_check(h, hipStreamCreateWithFlags(&h->commStream, hipStreamNonBlocking), "comm stream")) ||
+            (rc = hip_check(h, hipEventCreateWithFlags(&h->evRestrict, hipEventDisableTiming), "event")) ||
+            (rc = hip_check(h, hipEventCreateWithFlags(&h->evGathered, hipEventDisableTiming), "event")))
+            return rc;
+    }
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    float* seg = P<float>(h->shardSeg);
+    float* gathered = P<float>(h->shardGathered);
+    if ((rc = mas_apply_shard_restrict(h, rank, world, d_r4, seg, s))) return rc;
+    if (world == 1 && !allgather) {
+        if ((rc = hip_check(h, hipMemcpyAsync(gathered, seg, segBytes, hipMemcpyDeviceToDevice, s), "segment copy")))
+            return rc;
+        return mas_apply_shard_finish(h, rank, world, gathered, d_r4, d_z4, s);
+    }
+    if ((rc = hip_check(h, hipEventRecord(h->evRestrict, s), "record")) ||
+        (rc = hip_check(h, hipStreamWaitEvent(h->commStream, h->evRestrict, 0), "comm wait")))
+        return rc;
+    if (int e = allgather(seg, gathered, segBytes, h->commStream, user))
+        return fail(h, MAS_ERR_COMM, "allgather hook returned " + std::to_string(e));
+    if ((rc = hip_check(h, hipEventRecord(h->evGathered, h->commStream), "record")) ||
+        (rc = mas_apply_shard_fine(h, rank, world, d_r4, d_z4, s)) ||
+        (rc = hip_check(h, hipStreamWaitEvent(s, h->evGathered, 0), "gather wait")))
+        return rc;
+    return mas_apply_shard_complete(h, rank, world, gathered, d_z4, s);
 }
 
 }  // extern "C"

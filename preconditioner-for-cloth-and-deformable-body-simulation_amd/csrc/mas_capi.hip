@@ -128,6 +128,13 @@ int mas_destroy(mas_handle h) {
     for (auto& e : h->prof) hipEventDestroy(e);
     if (h->evFork) hipEventDestroy(h->evFork);
     if (h->evJoin) hipEventDestroy(h->evJoin);
+    release_comm(h);
+    if (h->commStream) {
+        hipStreamSynchronize(h->commStream);
+        hipStreamDestroy(h->commStream);
+    }
+    if (h->evRestrict) hipEventDestroy(h->evRestrict);
+    if (h->evGathered) hipEventDestroy(h->evGathered);
     if (h->stream2) {
         hipStreamSynchronize(h->stream2);
         hipStreamDestroy(h->stream2);

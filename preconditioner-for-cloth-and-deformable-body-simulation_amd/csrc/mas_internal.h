@@ -105,6 +105,13 @@ struct mas_context {
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
     std::vector<int> l1First;  // first level-1 local id per level-0 bank (+ n1), for sharding
     int shardWorld = 0;
+    // one-call sharded apply (mas_shard_apply_device): library-owned segments,
+    // the communication stream and its fork/join events
+    mas::Buffer shardSeg, shardGathered;
+    hipStream_t commStream = nullptr;
+    hipEvent_t evRestrict = nullptr, evGathered = nullptr;
+    void* rcclComm = nullptr;  // ncclComm_t (comm_rccl.hip)
+    int rcclRank = -1, rcclWorld = 0;
     hipEvent_t* shardPendingEv = nullptr;  // profiling events of an overlapped sharded apply in flight
     // staging for host-pointer entry points
     mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
@@ -124,7 +131,7 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &tileSlot, &valuSlot, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -162,6 +169,7 @@ int build_chain_tables(mas_context* h, hipStream_t s);
 void launch_coarse_chain(mas_context* h, const float4* r, hipStream_t s);
 void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s);
 int compute_l1_first(mas_context* h, hipStream_t s);
+void release_comm(mas_context* h);  // comm_rccl.hip
 int copy_block_inverse(mas_context* h, int blk, float* out96);
 int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,
             const float4* d_b, int maxIters, float tol, int precondition, mas_pcg_result* res, hipStream_t s);

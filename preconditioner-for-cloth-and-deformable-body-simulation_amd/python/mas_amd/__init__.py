@@ -26,14 +26,19 @@ FACADE_PATH = os.path.join(LIB_DIR, "libSeSchwarzPreconditioner.so")
 
 MAS_OK = 0
 STATUS = {0: "MAS_OK", -1: "MAS_ERR_ARG", -2: "MAS_ERR_HIP", -3: "MAS_ERR_CAPACITY", -4: "MAS_ERR_STATE",
-          -5: "MAS_ERR_LEVELS", -6: "MAS_ERR_NOMEM", -7: "MAS_ERR_NO_DEVICE"}
+          -5: "MAS_ERR_LEVELS", -6: "MAS_ERR_NOMEM", -7: "MAS_ERR_NO_DEVICE", -8: "MAS_ERR_COMM"}
+
+# mas_allgather_fn(send, recv, bytes, stream, user) -> int
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                ctypes.c_void_p)
 
 # every entry point declared in include/mas_capi.h
 EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_allocate", "mas_prepare",
            "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_get_info",
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
            "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
-           "mas_apply_shard_fine", "mas_apply_shard_complete",
+           "mas_apply_shard_fine", "mas_apply_shard_complete", "mas_shard_apply_device", "mas_rccl_unique_id",
+           "mas_rccl_init", "mas_shard_apply_rccl",
            "mas_pcg_solve_device", "mas_pcg_solve", "mas_blob_size", "mas_save_blob", "mas_load_blob",
            "mas_blob_validate"]
 
@@ -120,6 +125,10 @@ def lib():
         L.mas_apply_shard_finish.argtypes = [P, I, I, P, P, P, P]
         L.mas_apply_shard_fine.argtypes = [P, I, I, P, P, P]
         L.mas_apply_shard_complete.argtypes = [P, I, I, P, P, P]
+        L.mas_shard_apply_device.argtypes = [P, I, I, ALLGATHER_FN, P, P, P, P]
+        L.mas_rccl_unique_id.argtypes = [P]
+        L.mas_rccl_init.argtypes = [P, P, I, I]
+        L.mas_shard_apply_rccl.argtypes = [P, P, P, P]
         F = ctypes.c_float
         L.mas_pcg_solve_device.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result), P]
         L.mas_pcg_solve.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result)]
@@ -326,6 +335,41 @@ class SeSchwarzPreconditioner:
         self._check(self._L.mas_apply_shard_complete(self.h, rank, world, _ptr(gathered), _ptr(z), _ptr(stream)),
                     "shard_complete")
 
+    def shard_apply(self, rank, world, z, r, allgather=None, stream=None):
+        """One call per rank and apply (mas_shard_apply_device): restrict, the
+        allgather hook on the library's communication stream while the own
+        level-0 blocks run, then the coarse levels + prolongation.
+        allgather(send_ptr, recv_ptr, nbytes, stream_ptr) -> None enqueues the
+        gather on that stream (raise to fail); None only for world == 1."""
+        v = self._shard_vecs(rank, world, r=r, z=z)
+        r, z = v["r"], v["z"]
+        err = []
+
+        def hook(send, recv, nbytes, strm, _user):
+            try:
+                allgather(send, recv, nbytes, strm)
+                return 0
+            except Exception as e:  # reported as MAS_ERR_COMM
+                err.append(e)
+                return 1
+
+        fn = ALLGATHER_FN(hook) if allgather is not None else ALLGATHER_FN()
+        rc = self._L.mas_shard_apply_device(self.h, rank, world, fn, None, _ptr(z), _ptr(r), _ptr(stream))
+        if err:
+            raise MasError(f"shard_apply: allgather hook failed: {err[0]!r}") from err[0]
+        self._check(rc, "shard_apply")
+
+    def rccl_init(self, unique_id: bytes, rank, world):
+        """Give the handle its own RCCL communicator (mas_rccl_init)."""
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        self._check(self._L.mas_rccl_init(self.h, buf, rank, world), "rccl_init")
+
+    def shard_apply_rccl(self, z, r, stream=None):
+        """mas_shard_apply_rccl: the one-call sharded apply over the handle's RCCL communicator."""
+        z = _dev(z, self._nV, 4, "float32", "z")
+        r = _dev(r, self._nV, 4, "float32", "r")
+        self._check(self._L.mas_shard_apply_rccl(self.h, _ptr(z), _ptr(r), _ptr(stream)), "shard_apply_rccl")
+
     # ---- GPU-resident PCG (include/mas_capi.h, SURVEY 8(f) 1) ----
     def pcg_solve(self, diagonal, csrOffDiagonals, csrRanges, b, x0=None, max_iters=1000, tol=1e-5,
                   precondition=True):
@@ -434,6 +478,15 @@ def from_mesh(mesh, max_levels=0, contacts=None, **kw) -> SeSchwarzPreconditione
         vf, vfC = contacts
         P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, vf, None, None, vfC)
     return P
+
+
+def rccl_unique_id() -> bytes:
+    """mas_rccl_unique_id: 128 bytes for rank 0 to broadcast before rccl_init."""
+    buf = ctypes.create_string_buffer(128)
+    rc = lib().mas_rccl_unique_id(buf)
+    if rc != MAS_OK:
+        raise MasError(f"mas_rccl_unique_id failed: {STATUS.get(rc, rc)}")
+    return buf.raw
 
 
 def blob_validate(blob) -> int:

@@ -94,3 +94,119 @@ def test_sharded_apply_helper_overlap_world1():
         S(z, r, s)
         s.synchronize()
         assert np.array_equal(z.cpu().numpy(), P.Preconditioning(None, r.cpu().numpy())), overlap
+
+
+def _unsharded(P, r):
+    import torch
+    z = torch.zeros_like(r)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    P.PreconditioningDevice(z, r, s.cuda_stream)
+    s.synchronize()
+    return z
+
+
+@pytest.mark.parametrize("kind,W,L,worlds,nc", [("cloth", 100, 3, (1, 2, 3), 0), ("tet", 16, 3, (2, 8), 0),
+                                                ("cloth", 1024, 4, (8,), 100_000)])
+def test_one_call_shard_apply_bitwise(kind, W, L, worlds, nc):
+    """mas_shard_apply_device (the collective inside the library, the level-0
+    solves overlapping it on the apply stream): with an in-process allgather
+    hook -- it writes every rank's segment into `recv` through the step-wise
+    restrict, so all ranks' calls run in one process -- the union of the
+    ranks' own z entries equals the unsharded apply bitwise."""
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    from mas_amd.distributed import device_view
+    mesh = cloth(W) if kind == "cloth" else tet(W)
+    contacts = meshgen.vf_contacts(mesh, nc, seed=3) if nc else None
+    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 8)).cuda()
+    z_ref = _unsharded(P, r)
+    s = torch.cuda.Stream()
+    for world in worlds:
+        calls = []
+
+        def hook(send, recv, nbytes, strm):
+            n = nbytes // 16
+            calls.append(nbytes)
+            dst = device_view(recv, 4 * n * world, r.device).view(world, n, 4)
+            for g in range(world):  # every rank's segment, as an allgather would deliver it
+                P.shard_restrict(g, world, r, dst[g], strm)
+
+        z = torch.full_like(r, float("nan"))
+        for g in range(world):
+            P.shard_apply(g, world, z, r, allgather=hook if world > 1 else None, stream=s.cuda_stream)
+        s.synchronize()
+        assert torch.equal(z, z_ref), (world, float((z - z_ref).abs().max()))
+        assert len(calls) == (world if world > 1 else 0)
+
+
+def test_one_call_shard_apply_errors():
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(40)
+    P = mas_amd.from_mesh(mesh)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 1)).cuda()
+    z = torch.zeros_like(r)
+    with pytest.raises(mas_amd.MasError, match="ARG"):
+        P.shard_apply(0, 2, z, r)  # no allgather for world 2
+
+    def broken(*a):
+        raise RuntimeError("link down")
+
+    with pytest.raises(mas_amd.MasError, match="link down"):
+        P.shard_apply(1, 2, z, r, allgather=broken)
+    with pytest.raises(mas_amd.MasError, match="STATE"):
+        P.shard_apply_rccl(z, r)  # no communicator yet
+
+
+def test_rccl_transport_world1():
+    """The library's own RCCL communicator (dlopen'd librccl, mas_rccl_init)
+    on a one-rank world: same z as the unsharded apply."""
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    from mas_amd.distributed import ShardedApply
+    mesh = cloth(100)
+    P = mas_amd.from_mesh(mesh, max_levels=3)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 12)).cuda()
+    z_ref = _unsharded(P, r)
+    S = ShardedApply(P, 0, 1, transport="rccl")
+    z = torch.zeros_like(r)
+    s = torch.cuda.Stream()
+    for _ in range(3):
+        S(z, r, s)
+    s.synchronize()
+    assert torch.equal(z, z_ref)
+    # and an allgather over a one-rank RCCL communicator through mas_shard_apply_device's hook path
+    z2 = torch.zeros_like(r)
+    P.shard_apply_rccl(z2, r, s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(z2, z_ref)
+
+
+def test_two_processes_gloo_drive_library():
+    """Two ranks as two processes on this GPU, gloo allgather hook: each rank
+    runs the library's one-call sharded apply (its own handle, kernels on the
+    GPU) and checks its own z entries bitwise against its unsharded apply."""
+    import os
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29611", WORLD_SIZE="2")
+    procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "shard_worker.py")],
+                              env=dict(env, RANK=str(g), LOCAL_RANK="0"), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for g in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-3000:]
+        assert "SHARD_OK" in out, out[-3000:]
