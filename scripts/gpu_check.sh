@@ -6,9 +6,10 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-check}
 mkdir -p $O
 export TMPDIR=/tmp
-K=${2:+-k "$2"}
+K=()
+[ -n "$2" ] && K=(-k "$2")
 cd $R && \
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K > $O/pytest_gpu.log 2>&1 && \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > $O/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
 rc=$?
