@@ -144,6 +144,9 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="sharded path: replay one captured HIP graph per step (measured slower than eager "
                          "launches on one GPU at 1M and 256k: profiles/round1/ab/shard_overhead.json)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "torch"],
+                    help="sharded path: the handle's own RCCL communicator (mas_shard_apply_rccl, one library "
+                         "call per apply) or an allgather hook through torch.distributed")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo only to exercise N>1 on one GPU")
     args = ap.parse_args()
@@ -212,7 +215,13 @@ def main():
     use_graph = False
     if sharded_path:  # Morton-range shards + one RCCL allgather per apply
         from mas_amd.distributed import ShardedApply
-        sharded = ShardedApply(P, rank, world, device=torch.device("cuda", local))
+        transport = args.transport if args.dist_backend == "nccl" else "torch"
+        try:
+            sharded = ShardedApply(P, rank, world, device=torch.device("cuda", local), transport=transport)
+        except Exception as e:  # the library's RCCL could not start: the torch hook still shards
+            log(f"rccl transport unavailable ({e!r}); using the torch.distributed allgather hook")
+            transport = "torch"
+            sharded = ShardedApply(P, rank, world, device=torch.device("cuda", local), transport=transport)
         plan = sharded.plan
         use_graph = args.graph and args.dist_backend == "nccl"
 
@@ -220,6 +229,7 @@ def main():
             sharded(z, r, stream)
     else:
         plan = None
+        transport = None
 
         def step():
             P.PreconditioningDevice(z, r, sptr)
@@ -321,7 +331,9 @@ def main():
             "blocks": info["num_blocks"],
             "fine_blocks": info["num_fine_blocks"],
             "contact_stencils": info["num_stencils"],
-            "parallelism": (f"{world} Morton-range shards, {args.dist_backend} allgather of level-1 segments"
+            "parallelism": (f"{world} Morton-range shards, allgather of level-1 segments via "
+                            + ("the library's RCCL communicator (mas_shard_apply_rccl)" if transport == "rccl"
+                               else f"a torch.distributed {args.dist_backend} hook (mas_shard_apply_device)")
                             + (", HIP-graph replay" if use_graph else ", eager launches")
                             if sharded_path else "single-gpu"),
         },

@@ -94,15 +94,21 @@ class ShardedApply:
         self.P.shard_finish(self.rank, self.world, self.gathered, r, z, s.cuda_stream)
 
     def capture(self, z, r, stream):
-        """Record one apply (restrict, RCCL allgather, finish) as a HIP graph:
-        later calls with the same z, r replay it (removes the per-kernel host
-        launch cost).  Call after at least one eager apply."""
+        """Record one apply as a HIP graph: later calls with the same z, r
+        replay it (removes the per-kernel host launch cost).  The rccl
+        transport captures the one-call apply itself (the gather on the
+        library's communication stream, forked and joined inside the graph);
+        the torch transport captures the step-wise form.  Call after at least
+        one eager apply (buffers and tables exist by then)."""
         if self.world > 1 and self.backend == "gloo":
             raise RuntimeError("graph capture needs the nccl (RCCL) backend")
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=stream):
-            self._step_explicit(z, r, stream)
+            if self.transport == "rccl":
+                self._call(z, r, stream)
+            else:
+                self._step_explicit(z, r, stream)
         torch.cuda.synchronize()
         self.graph, self.graph_args = g, (z.data_ptr(), r.data_ptr())
 

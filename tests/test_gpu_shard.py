@@ -185,6 +185,16 @@ def test_rccl_transport_world1():
     P.shard_apply_rccl(z2, r, s.cuda_stream)
     s.synchronize()
     assert torch.equal(z2, z_ref)
+    # the one-call apply captured as a HIP graph (comm stream forked and joined inside) and replayed
+    z3 = torch.zeros_like(r)
+    S(z3, r, s)
+    S.capture(z3, r, s)
+    z3.zero_()
+    torch.cuda.synchronize()
+    for _ in range(2):
+        S(z3, r, s)
+    s.synchronize()
+    assert torch.equal(z3, z_ref)
 
 
 def test_two_processes_gloo_drive_library():
