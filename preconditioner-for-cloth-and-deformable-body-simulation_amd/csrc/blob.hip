@@ -156,18 +156,25 @@ static bool blob_maps_valid(const MasBlobHeader& hd, const unsigned char* in, co
     for (int v = 0; v < nV; ++v) {
         if (s2o[v] < 0 || s2o[v] >= nV || seen[s2o[v]]++ || o2s[s2o[v]] != v) return false;
     }
+    // goingNext of the real nodes below the top level: into the next level's
+    // real nodes (top-level and padding entries are never followed)
     const int* gn = arr(kSecGoingNext);
-    for (int i = 0; i < tc; ++i)  // the top level points at the sentinel total (.cpp:1244)
-        if (gn[i] < 0 || gn[i] > tc) return false;
+    for (int l = 0; l + 1 < L; ++l) {
+        const int b = l == 0 ? 0 : ls[2 * l + 1], nb = ls[2 * (l + 1) + 1];
+        for (int i = b; i < b + count(l); ++i)
+            if (gn[i] < nb || gn[i] >= nb + count(l + 1)) return false;
+    }
     const int* cst = arr(kSecCst);
     for (int l = 0; l < L; ++l)
         for (int v = 0; v < nV; ++v) {
             const int c = cst[(size_t)l * nV + v];
             if (c < 0 || (l + 1 < L && c >= count(l + 1))) return false;
         }
-    const int* ct = arr(kSecCoarseTables);
-    for (size_t i = 0; i < (size_t)nV * 4; ++i)
-        if (ct[i] < 0 || ct[i] >= tc) return false;
+    const int* ct = arr(kSecCoarseTables);  // ancestors of levels 1 .. L-1 (Int4, .cpp:1119-1147)
+    for (int v = 0; v < nV; ++v)
+        for (int l = 1; l < L && l <= 4; ++l)
+            if (ct[4 * (size_t)v + l - 1] < ls[2 * l + 1] || ct[4 * (size_t)v + l - 1] >= ls[2 * l + 1] + count(l))
+                return false;
     // per-vertex apply map {s2o, a1, a2, a3}: ancestors of the prolonged levels
     const int4* vm = reinterpret_cast<const int4*>(in + sec[kSecVmap]->offset);
     const int np = L < 4 ? L : 4;

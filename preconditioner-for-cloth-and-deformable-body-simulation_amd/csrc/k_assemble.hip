@@ -70,140 +70,161 @@ __device__ __forceinline__ void add_colmajor(float* e, const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// contacts (reference semantics, fp32 atomics)
+// contacts (deterministic, the reference's single-thread order)
 // ---------------------------------------------------------------------------
+//
+// PrepareCollisionHessian (.cpp:1201-1227) runs stencil by stencil: first
+// additional[idx[it]] += h w_it^2 for every vertex of the stencil, then per
+// pair (a, b) in order AdditionalSchwarzHessian2 (.cpp:1164-1199): at the
+// first level where both ids share a bank, block entry (my, ot) += t then
+// (ot, my) += t (t = w_a w_b h, the same matrix both times), and below the top
+// level additional[parent] += t for both parents (2t when they coincide).
+// PrepareHessian (.cpp:1229-1345) then pushes every coarse additional[x], x
+// ascending, into x's own diagonal and every ancestor's, and only then adds
+// the CSR terms.  The reference does the contact sums with float atomics
+// (order-free with threads, B-10); at CPU_THREAD_NUM = 1 they are these
+// ordered left folds, which is what is computed here:
+//   k_contact_count / _write  per stencil, its records in stencil order: a
+//                 block-entry record (key (my, ot)) per pair half, an
+//                 additional record (key node) per w^2 term and parent term;
+//                 values stored column-major, 9 floats
+//   radix sort    stable by key, so a key's records stay in stencil order
+//   fine entries  (rows < begin_1) are added by k_level0_block into its LDS
+//                 tile before the CSR terms
+//   coarse entries, additional rows: k_fold_runs_t folds each key's run left
+//                 from the zeroed target
+//   pushes        per coarse node x with an additional row: records (target,
+//                 x) for x and each ancestor, sorted stably by target (x
+//                 ascending), folded into the target's diagonal
+// Contact-free inputs skip all of it.
 
-// Two passes over the stencils: ADDITIONAL (the per-vertex w^2 h terms and
-// the parent terms, read by the level-0 assembly and k_additional_up) runs
-// first; PAIRS (the h w_a w_b terms into the blocks) runs after the level-0
-// blocks are written whole, so the fine blocks need no memset and no
-// read-back.  For the fine entries this adds the contact terms after the CSR
-// terms instead of before (.cpp:1201-1271): a reassociation of fp32 sums the
-// reference's multi-threaded atomics do not fix either (B-10).
-enum { kContactAdditional = 1, kContactPairs = 2 };
-constexpr int kContactThreads = 1024, kContactBlocks = 256;
-// Random contact pairs mostly meet only in the top level's single block, so
-// every stencil's 18 atomics per pair hit the same 9 216 floats of one dense
-// block (and, for pairs meeting one level lower, the 288 floats of the top
-// nodes' additional terms): 10.8 M same-address float atomics for 100k VF
-// contacts, 0.6 ms per pass.  When the top level is one block, each
-// workgroup therefore accumulates those targets in LDS (LDS float atomics)
-// and adds its partial sums to HBM once at the end (kContactBlocks
-// workgroups, so that many global adds per target).  Other targets are added
-// directly.  Sums of contact terms are atomic (order-free) in the reference
-// too (B-10).
-// Sixteen lanes per stencil, lane e < 9 owning entry (e / 3, e % 3) of every
-// 3x3 term: a wave's atomic instruction then covers 4 targets x 9 floats in
-// 12-36-byte runs.  With a thread per stencil each instruction sent 64 lanes
-// to 64 different cache lines, the slowest shape of global atomics (~17x below
-// contiguous, MI355X_MICROARCH.md atomics table): 341 us per pass at 100k VF.
-constexpr int kLanesPerStencil = 16;
-__global__ __launch_bounds__(kContactThreads) void k_collision_hessian(const DevStencil* __restrict__ st, int n,
-                                                                       int mode, const int* __restrict__ gn, int L,
-                                                                       int topNode, float* __restrict__ dense,
-                                                                       float* __restrict__ additional) {
-    __shared__ float priv[kDenseFloats];  // the top block (pairs) or the top nodes' additional terms (288)
-    const bool privatize = topNode >= 0;
-    const unsigned topBank = privatize ? (unsigned)topNode >> 5 : 0xffffffffu;
-    const int nPriv = mode == kContactPairs ? kDenseFloats : 32 * 9;
-    if (privatize)
-        for (int e = threadIdx.x; e < nPriv; e += blockDim.x) priv[e] = 0.f;
-    __syncthreads();
-    const int e = threadIdx.x % kLanesPerStencil, r = e / 3, c = e % 3;
-    const int perGrid = gridDim.x * (blockDim.x / kLanesPerStencil);
-    for (int i = blockIdx.x * (blockDim.x / kLanesPerStencil) + threadIdx.x / kLanesPerStencil; i < n; i += perGrid) {
-        if (e >= 9) continue;
-        const DevStencil& s = st[i];  // read in place: a private copy indexed by it/a/b would live in scratch
-        // OuterProduct(d, d * stiff), SeMatrix.h:352-363: entry (r, c) = d_r (d_c stiff)
-        const float hm = __fmul_rn(s.dir[r], __fmul_rn(s.dir[c], s.stiff));
-        for (int it = 0; mode == kContactAdditional && it < s.n; ++it)  // .cpp:1214-1217: additional[idx] += h w^2
-            atomicAdd(additional + 9 * (size_t)s.idx[it] + e, __fmul_rn(hm, __fmul_rn(s.w[it], s.w[it])));
-        for (int a = 0; a < s.n; ++a)  // AdditionalSchwarzHessian2, .cpp:1164-1199
-            for (int b = a + 1; b < s.n; ++b) {
-                const float t = __fmul_rn(__fmul_rn(s.w[a], s.w[b]), hm);
-                unsigned my = (unsigned)s.idx[a], ot = (unsigned)s.idx[b];
-                const int level = climb(gn, L, my, ot);
-                if (level >= L) continue;
-                // LDS and HBM targets on separate paths: one pointer that may be
-                // either compiles to flat atomics, which serialise on LDS
-                if (mode == kContactPairs) {
-                    if ((my >> 5) == topBank) {
-                        atomicAdd(&priv[(3 * (my & 31) + r) * 96 + 3 * (ot & 31) + c], t);
-                        atomicAdd(&priv[(3 * (ot & 31) + r) * 96 + 3 * (my & 31) + c], t);
-                    } else {
-                        atomicAdd(entry(dense, my, ot) + r * 96 + c, t);
-                        atomicAdd(entry(dense, ot, my) + r * 96 + c, t);
-                    }
-                } else if (level < L - 1) {
-                    const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
-                    if ((pm >> 5) == topBank) {  // then po is a top node too
-                        if (pm == po) {
-                            atomicAdd(&priv[9 * (pm & 31) + e], __fmul_rn(t, 2.0f));
-                        } else {
-                            atomicAdd(&priv[9 * (pm & 31) + e], t);
-                            atomicAdd(&priv[9 * (po & 31) + e], t);
-                        }
-                    } else if (pm == po) {
-                        atomicAdd(additional + 9 * (size_t)pm + e, __fmul_rn(t, 2.0f));
-                    } else {
-                        atomicAdd(additional + 9 * (size_t)pm + e, t);
-                        atomicAdd(additional + 9 * (size_t)po + e, t);
-                    }
-                }
-            }
-    }
-    if (!privatize) return;
-    __syncthreads();
-    float* dst = mode == kContactPairs ? dense + (size_t)topBank * kDenseFloats : additional + 9 * (size_t)(topBank * 32);
-    for (int q = threadIdx.x; q < nPriv; q += blockDim.x)
-        if (priv[q] != 0.f) atomicAdd(dst + q, priv[q]);
+__device__ __forceinline__ void contact_h(const DevStencil& s, float (&hm)[9]) {
+    // OuterProduct(d, d * stiff), SeMatrix.h:352-363; column-major: hm[c * 3 + r] = d_r (d_c stiff)
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) hm[c * 3 + r] = __fmul_rn(s.dir[r], __fmul_rn(s.dir[c], s.stiff));
 }
 
-// .cpp:1236-1252: coarse additional -> own diagonal and every ancestor.
-// Contact terms of coarse nodes reach their own diagonal and every ancestor's
-// (.cpp:1214-1217 then the hierarchy climb): diag(P) += S(P), where S(P) is
-// add(P) plus the S of P's children.  Adding add(c) to each ancestor with one
-// atomic per level (the first form) put ~33k same-address atomics on the top
-// node (86 us).  Instead S climbs one level per launch: the children of a
-// level-l node all sit in one 32-node bank of level l-1 (a level-l node is a
-// component of such a bank), so one half-wave per child bank sums S over the
-// children of each parent in lane order and the lowest child writes
-// S(parent) = add(parent) + sum into `additional` (in place) and adds it to the
-// parent's diagonal -- a single writer per target, no atomics.  (Sums of
-// contact terms are order-free in the reference, B-10.)
-__global__ __launch_bounds__(64) void k_additional_up(int beginC, int nC, int tc, bool ownDiag,
-                                                      const int* __restrict__ gn, float* __restrict__ additional,
-                                                      float* __restrict__ dense) {
-    __shared__ float S[64][9];
-    __shared__ int par[64];
-    const int t = threadIdx.x, c = beginC + blockIdx.x * 64 + t;
-    const bool live = c < beginC + nC;
-    const int p = live ? gn[c] : -1;
-    float a[9];
-    for (int e = 0; e < 9; ++e) a[e] = live ? additional[9 * (size_t)c + e] : 0.f;
-    if (live && ownDiag) {  // level-1 nodes: their own diagonal
-        float* d = entry(dense, c, c);
-        for (int r = 0; r < 3; ++r)
-            for (int q = 0; q < 3; ++q) d[r * 96 + q] = __fadd_rn(d[r * 96 + q], a[r * 3 + q]);
+// counts: dCnt[i] block-entry records, aCnt[i] additional records of stencil i
+__global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restrict__ st, int n,
+                                                       const int* __restrict__ gn, int L, int* __restrict__ dCnt,
+                                                       int* __restrict__ aCnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {  // closes the exclusive scans
+        dCnt[n] = aCnt[n] = 0;
+        return;
     }
-    for (int e = 0; e < 9; ++e) S[t][e] = a[e];
-    par[t] = p;
-    __syncthreads();
-    if (!live || p >= tc) return;
-    const int b0 = t & ~31;
-    for (int j = b0; j < t; ++j)
-        if (par[j] == p) return;  // not the lowest child of p
-    float sum[9];
-    for (int e = 0; e < 9; ++e) sum[e] = additional[9 * (size_t)p + e];
-    for (int j = t; j < b0 + 32; ++j)
-        if (par[j] == p)
-            for (int e = 0; e < 9; ++e) sum[e] = __fadd_rn(sum[e], S[j][e]);
-    float* d = entry(dense, p, p);
-    for (int r = 0; r < 3; ++r)
-        for (int q = 0; q < 3; ++q) {
-            additional[9 * (size_t)p + r * 3 + q] = sum[r * 3 + q];
-            d[r * 96 + q] = __fadd_rn(d[r * 96 + q], sum[r * 3 + q]);
+    const DevStencil s = st[i];
+    int d = 0, a = s.n;
+    for (int x = 0; x < s.n; ++x)
+        for (int y = x + 1; y < s.n; ++y) {
+            unsigned my = (unsigned)s.idx[x], ot = (unsigned)s.idx[y];
+            const int level = climb(gn, L, my, ot);
+            if (level >= L) continue;
+            d += 2;
+            if (level < L - 1) a += gn[my] == gn[ot] ? 1 : 2;
         }
+    dCnt[i] = d;
+    aCnt[i] = a;
+}
+
+// The records of stencil i at dOff[i] / aOff[i], in the reference's order;
+// keys: block entry (my << B) | ot, additional node id.
+__global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restrict__ st, int n,
+                                                       const int* __restrict__ gn, int L, int B,
+                                                       const int* __restrict__ dOff, const int* __restrict__ aOff,
+                                                       unsigned long long* __restrict__ dKeys, int* __restrict__ dIds,
+                                                       float* __restrict__ dVal, unsigned* __restrict__ aKeys,
+                                                       int* __restrict__ aIds, float* __restrict__ aVal) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const DevStencil s = st[i];
+    float hm[9];
+    contact_h(s, hm);
+    int d = dOff[i], a = aOff[i];
+    for (int it = 0; it < s.n; ++it, ++a) {  // .cpp:1214-1217: additional[idx] += h w^2
+        const float w2 = __fmul_rn(s.w[it], s.w[it]);
+        aKeys[a] = (unsigned)s.idx[it];
+        aIds[a] = a;
+        for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = __fmul_rn(hm[e], w2);
+    }
+    for (int x = 0; x < s.n; ++x)
+        for (int y = x + 1; y < s.n; ++y) {
+            unsigned my = (unsigned)s.idx[x], ot = (unsigned)s.idx[y];
+            const int level = climb(gn, L, my, ot);
+            if (level >= L) continue;
+            const float ww = __fmul_rn(s.w[x], s.w[y]);
+            float t[9];
+            for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e]);
+            // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot]
+            dKeys[d] = ((unsigned long long)my << B) | ot;
+            dKeys[d + 1] = ((unsigned long long)ot << B) | my;
+            dIds[d] = d;
+            dIds[d + 1] = d + 1;
+            for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
+            d += 2;
+            if (level < L - 1) {
+                const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
+                if (pm == po) {
+                    aKeys[a] = pm;
+                    aIds[a] = a;
+                    for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = __fmul_rn(t[e], 2.0f);
+                    ++a;
+                } else {
+                    aKeys[a] = pm;
+                    aKeys[a + 1] = po;
+                    aIds[a] = a;
+                    aIds[a + 1] = a + 1;
+                    for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = aVal[9 * (size_t)(a + 1) + e] = t[e];
+                    a += 2;
+                }
+            }
+        }
+}
+
+// Per level-0 block, the range of its contact block-entry records in the
+// sorted array (rows < begin_1 sort first): fineOff[b] .. fineOff[b + 1].
+__global__ __launch_bounds__(256) void k_contact_fine_bounds(int nD, int B, int begin1, int nFineBlk,
+                                                             const unsigned long long* __restrict__ keys,
+                                                             int* __restrict__ fineOff) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > nD) return;
+    auto blockOf = [&](int q) {
+        if (q >= nD) return nFineBlk;
+        const unsigned row = (unsigned)(keys[q] >> B);
+        return row < (unsigned)begin1 ? (int)(row >> 5) : nFineBlk;
+    };
+    const int b = blockOf(j), prev = j == 0 ? -1 : blockOf(j - 1);
+    for (int k = prev + 1; k <= b; ++k) fineOff[k] = j;  // blocks (prev, b] start here
+}
+
+// push records of coarse node x (a run start in the sorted additional keys):
+// targets x, gn[x], ... below total
+__global__ __launch_bounds__(256) void k_push_count(int nA, int begin1, int tc, const unsigned* __restrict__ aKeys,
+                                                    const int* __restrict__ gn, int* __restrict__ pCnt) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > nA) return;
+    int c = 0;
+    if (j < nA) {
+        const unsigned x = aKeys[j];
+        if (x >= (unsigned)begin1 && (j == 0 || aKeys[j - 1] != x))
+            for (int t = (int)x; t < tc; t = gn[t]) ++c;
+    }
+    pCnt[j] = c;
+}
+
+__global__ __launch_bounds__(256) void k_push_write(int nA, int begin1, int tc, const unsigned* __restrict__ aKeys,
+                                                    const int* __restrict__ gn, const int* __restrict__ pOff,
+                                                    unsigned* __restrict__ pKeys, int* __restrict__ pIds) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nA) return;
+    const unsigned x = aKeys[j];
+    if (x < (unsigned)begin1 || (j > 0 && aKeys[j - 1] == x)) return;
+    int w = pOff[j];
+    for (int t = (int)x; t < tc; t = gn[t], ++w) {
+        pKeys[w] = (unsigned)t;
+        pIds[w] = (int)x;  // the pushed value: additional row x (row-major)
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -225,19 +246,42 @@ __global__ __launch_bounds__(64) void k_additional_up(int beginC, int nC, int tc
 // zero block, drains, then each lane stores its 3x3 entries straight to HBM --
 // 749 vs 338 us at 1M (the 12-byte scattered stores are partial-line writes);
 // persistent workgroups (4 per CU) looping over blocks -- 355 us.
+// Contact block entries of this block (sorted, each entry's records in
+// stencil order) are added to the zero tile first, lane e < 9 owning
+// component e of every entry -- the reference adds PrepareCollisionHessian's
+// terms before PrepareHessian's (.cpp:88-97).
+struct FineContacts {
+    const unsigned long long* keys;  // sorted block-entry keys (row << B) | col
+    const int* ids;                  // record index -> 9 column-major floats in val
+    const float* val;
+    const int* off;                  // per level-0 block: first record (nFineBlk + 1)
+    int B;
+};
+
 __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* __restrict__ s2o,
                                                      const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                      const float* __restrict__ diag9,
                                                      const float* __restrict__ off9, const int* __restrict__ ranges,
                                                      const float* __restrict__ additional,
                                                      float* __restrict__ dense, float* __restrict__ od,
-                                                     int* __restrict__ recCnt) {
+                                                     int* __restrict__ recCnt, FineContacts fc) {
     __shared__ __attribute__((aligned(16))) float tile[kDenseFloats];
     const int lane = threadIdx.x;
     const size_t blk = blockIdx.x;
     float4* gblk = reinterpret_cast<float4*>(dense + blk * kDenseFloats);
     float4* t4 = reinterpret_cast<float4*>(tile);
     for (int q = lane; q < kDenseFloats / 4; q += 64) t4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    if (fc.off && lane < 9) {
+        const int r = lane / 3, c = lane % 3;
+        const int j1 = fc.off[blk + 1];
+        for (int j = fc.off[blk]; j < j1; ++j) {
+            const unsigned long long k = fc.keys[j];
+            const unsigned row = (unsigned)(k >> fc.B), col = (unsigned)(k & ((1ull << fc.B) - 1));
+            float* e = tile + (3 * (row & 31) + r) * 96 + 3 * (col & 31) + c;
+            *e = __fadd_rn(*e, fc.val[9 * (size_t)fc.ids[j] + c * 3 + r]);
+        }
+    }
     __syncthreads();
     const int n = lane;
     const int v = (int)blk * 32 + n;
@@ -387,29 +431,53 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, RecKey rk, const
 // atomics on one address serialised and cost ~300 us.)
 constexpr int kLongRun = 16, kFoldBatch = 8;
 
+// Fold targets: where the 3x3 of a key lives and its row stride.
+struct DenseEntry {  // block entry (row node, column node) of the dense buffer
+    float* dense;
+    RecKey rk;
+    static constexpr int kStride = 96;
+    __device__ float* at(unsigned long long k) const { return entry(dense, rk.row(k), rk.col(k)); }
+};
+struct DenseDiag {  // the diagonal entry of a node
+    float* dense;
+    static constexpr int kStride = 96;
+    __device__ float* at(unsigned k) const { return entry(dense, k, k); }
+};
+struct NodeRow {  // a row-major 9-float row per node (additional)
+    float* base;
+    static constexpr int kStride = 3;
+    __device__ float* at(unsigned k) const { return base + 9 * (size_t)k; }
+};
+
 // One wave per 64 sorted positions: the lanes find the runs starting there;
 // each short-run lane folds its own run, then the wave folds the long runs one
 // after the other.  (Separate kernels for the two kinds measured 106 + 78 us
-// at 1M: each re-read the keys to find its runs.)
-__global__ __launch_bounds__(64) void k_fold_runs(int n, RecKey rk, const unsigned long long* __restrict__ keys,
-                                                  const int* __restrict__ mats, const float* __restrict__ off9,
-                                                  float* __restrict__ dense) {
-    __shared__ float T[9 * 65];  // T[q * 65 + record]: off9 component q; stride 65 keeps lanes 0..8 on distinct banks
+// at 1M: each re-read the keys to find its runs.)  Each run is folded onto
+// the target's current value in sorted (= stable, insertion) order; a record's
+// 3x3 is vals[9 id ...], column-major (off9, contact values) or row-major
+// (additional rows).  `dead` marks records to skip.
+template <class Tgt, bool kColMajor, class Key>
+__global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __restrict__ keys,
+                                                  const int* __restrict__ mats, const float* __restrict__ vals,
+                                                  Tgt tgt) {
+    __shared__ float T[9 * 65];  // T[q * 65 + record]: component q (row-major); stride 65 keeps lanes 0..8 apart
+    constexpr int S = Tgt::kStride;
+    auto comp = [](int r, int c) { return kColMajor ? c * 3 + r : r * 3 + c; };
     const int lane = threadIdx.x;
     const int i = blockIdx.x * 64 + lane;
     bool isStart = false, isLong = false;
-    unsigned long long key = 0;
+    Key key = 0;
     if (i < n) {
         key = keys[i];
-        isStart = key != rk.dead() && (i == 0 || keys[i - 1] != key);
+        isStart = key != dead && (i == 0 || keys[i - 1] != key);
         // sorted: a run starting at i has >= kLongRun records iff position i + kLongRun - 1 has its key
         isLong = isStart && i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key;
     }
     if (isStart && !isLong) {  // short run: this lane, loads batched kFoldBatch at a time
-        float* e = entry(dense, rk.row(key), rk.col(key));
+        float* e = tgt.at(key);
         float acc[9];
         for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
+            for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * S + c];
         for (int j0 = i; j0 < i + kLongRun; j0 += kFoldBatch) {
             bool in[kFoldBatch];
             float m[kFoldBatch][9];
@@ -417,7 +485,7 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, RecKey rk, const unsign
             for (int t = 0; t < kFoldBatch; ++t) {
                 const int j = j0 + t;
                 in[t] = j < n && keys[j] == key;
-                const float* src = off9 + 9 * (size_t)(in[t] ? mats[j] : mats[i]);
+                const float* src = vals + 9 * (size_t)(in[t] ? mats[j] : mats[i]);
 #pragma unroll
                 for (int q = 0; q < 9; ++q) m[t][q] = src[q];
             }
@@ -425,35 +493,35 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, RecKey rk, const unsign
             for (int t = 0; t < kFoldBatch; ++t)
                 if (in[t])
                     for (int r = 0; r < 3; ++r)
-                        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[t][c * 3 + r]);
+                        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], m[t][comp(r, c)]);
             if (!in[kFoldBatch - 1]) break;
         }
         for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
+            for (int c = 0; c < 3; ++c) e[r * S + c] = acc[r * 3 + c];
     }
     // long runs: the whole wave, 64 records per step staged in LDS, lanes 0..8 fold
     const int r = lane / 3, c = lane % 3;
     for (unsigned long long starts = __ballot(isLong); starts; starts &= starts - 1) {
         const int start = blockIdx.x * 64 + __ffsll((long long)starts) - 1;
-        const unsigned long long lkey = keys[start];
-        float* e = entry(dense, rk.row(lkey), rk.col(lkey));
-        float acc = lane < 9 ? e[r * 96 + c] : 0.f;
+        const Key lkey = keys[start];
+        float* e = tgt.at(lkey);
+        float acc = lane < 9 ? e[r * S + c] : 0.f;
         for (int j0 = start;; j0 += 64) {
             const int j = j0 + lane;
             const bool in = j < n && keys[j] == lkey;
             const int cnt = __popcll(__ballot(in));  // the run is contiguous: lanes 0..cnt-1
             if (in) {
-                const float* src = off9 + 9 * (size_t)mats[j];
+                const float* src = vals + 9 * (size_t)mats[j];
 #pragma unroll
                 for (int q = 0; q < 9; ++q) T[q * 65 + lane] = src[q];
             }
             __syncthreads();
             if (lane < 9)
-                for (int k = 0; k < cnt; ++k) acc = __fadd_rn(acc, T[(c * 3 + r) * 65 + k]);
+                for (int k = 0; k < cnt; ++k) acc = __fadd_rn(acc, T[comp(r, c) * 65 + k]);
             __syncthreads();
             if (cnt < 64) break;
         }
-        if (lane < 9) e[r * 96 + c] = acc;
+        if (lane < 9) e[r * S + c] = acc;
     }
 }
 
@@ -670,6 +738,110 @@ __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, 
     }
 }
 
+template <class T>
+static int exclusive_scan(mas_context* h, const T* in, T* out, int n, hipStream_t s, const char* what) {
+    size_t tmp = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, n, s);
+    int rc = ensure(h, h->cubTemp, tmp);
+    if (rc) return rc;
+    return hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, in, out, n, s), what);
+}
+
+template <class K>
+static int sort_pairs(mas_context* h, const K* kin, K* kout, const int* vin, int* vout, int n, int bits,
+                      hipStream_t s, const char* what) {
+    if (n <= 0) return MAS_OK;
+    size_t tmp = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, n, 0, bits, s);
+    int rc = ensure(h, h->cubTemp, tmp);
+    if (rc) return rc;
+    return hip_check(h, hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, kin, kout, vin, vout, n, 0, bits, s),
+                     what);
+}
+
+// The contact part of the assembly in the reference's single-thread order
+// (see "contacts" above): on return the coarse blocks hold the contact block
+// entries and the additional pushes, `additional` holds every node's contact
+// row, and fc points k_level0_block at the fine block entries.
+static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc) {
+    const int n = h->nStencil, L = h->L, tc = h->totalClusters, begin1 = L > 1 ? h->levelSize[3] : tc;
+    const int B = std::max(1, bit_width((unsigned)(tc - 1)));
+    const int* gn = P<int>(h->goingNext);
+    const DevStencil* st = P<DevStencil>(h->stencils);
+    int rc;
+    if ((rc = ensure(h, h->cdCnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->cdOff, (size_t)(n + 1) * 4)) ||
+        (rc = ensure(h, h->caCnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->caOff, (size_t)(n + 1) * 4)) ||
+        (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4)))
+        return rc;
+    k_contact_count<<<cdiv(n + 1, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdCnt), P<int>(h->caCnt));
+    if ((rc = exclusive_scan(h, P<int>(h->cdCnt), P<int>(h->cdOff), n + 1, s, "contact scan")) ||
+        (rc = exclusive_scan(h, P<int>(h->caCnt), P<int>(h->caOff), n + 1, s, "contact scan")))
+        return rc;
+    int tot[2] = {0, 0};
+    if ((rc = hip_check(h, hipMemcpyAsync(&tot[0], P<int>(h->cdOff) + n, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
+        (rc = hip_check(h, hipMemcpyAsync(&tot[1], P<int>(h->caOff) + n, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
+        (rc = hip_check(h, hipStreamSynchronize(s), "contact count sync")))
+        return rc;
+    const int nD = tot[0], nA = tot[1];
+    const size_t d1 = nD > 0 ? nD : 1, a1 = nA > 0 ? nA : 1;
+    if ((rc = ensure(h, h->cdKeys, d1 * 8)) || (rc = ensure(h, h->cdKeysS, d1 * 8)) ||
+        (rc = ensure(h, h->cdIds, d1 * 4)) || (rc = ensure(h, h->cdIdsS, d1 * 4)) ||
+        (rc = ensure(h, h->cdVal, d1 * 36)) || (rc = ensure(h, h->caKeys, a1 * 4)) ||
+        (rc = ensure(h, h->caKeysS, a1 * 4)) || (rc = ensure(h, h->caIds, a1 * 4)) ||
+        (rc = ensure(h, h->caIdsS, a1 * 4)) || (rc = ensure(h, h->caVal, a1 * 36)) ||
+        (rc = ensure(h, h->cpCnt, (a1 + 1) * 4)) || (rc = ensure(h, h->cpOff, (a1 + 1) * 4)))
+        return rc;
+    k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, gn, L, B, P<int>(h->cdOff), P<int>(h->caOff),
+                                                 P<unsigned long long>(h->cdKeys), P<int>(h->cdIds),
+                                                 P<float>(h->cdVal), P<unsigned>(h->caKeys), P<int>(h->caIds),
+                                                 P<float>(h->caVal));
+    if ((rc = sort_pairs(h, P<unsigned long long>(h->cdKeys), P<unsigned long long>(h->cdKeysS), P<int>(h->cdIds),
+                         P<int>(h->cdIdsS), nD, 2 * B, s, "contact entry sort")) ||
+        (rc = sort_pairs(h, P<unsigned>(h->caKeys), P<unsigned>(h->caKeysS), P<int>(h->caIds), P<int>(h->caIdsS), nA,
+                         B, s, "contact row sort")))
+        return rc;
+    float* dense = P<float>(h->dense);
+    // fine entries: k_level0_block; coarse entries: folded onto the zeroed coarse blocks
+    k_contact_fine_bounds<<<cdiv(nD + 1, 256), 256, 0, s>>>(nD, B, begin1, h->nFineBlk,
+                                                            P<unsigned long long>(h->cdKeysS), P<int>(h->cFineOff));
+    int fineEnd = 0;
+    if ((rc = hip_check(h, hipMemcpyAsync(&fineEnd, P<int>(h->cFineOff) + h->nFineBlk, 4, hipMemcpyDeviceToHost, s),
+                        "D2H")))
+        return rc;
+    // additional rows (level 0 and coarse), folded from zero
+    if (nA > 0)
+        k_fold_runs<NodeRow, true, unsigned><<<cdiv(nA, 64), 64, 0, s>>>(
+            nA, 0xffffffffu, P<unsigned>(h->caKeysS), P<int>(h->caIdsS), P<float>(h->caVal),
+            NodeRow{P<float>(h->additional)});
+    k_push_count<<<cdiv(nA + 1, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), gn, P<int>(h->cpCnt));
+    if ((rc = exclusive_scan(h, P<int>(h->cpCnt), P<int>(h->cpOff), nA + 1, s, "push scan"))) return rc;
+    int nP = 0;
+    if ((rc = hip_check(h, hipMemcpyAsync(&nP, P<int>(h->cpOff) + nA, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
+        (rc = hip_check(h, hipStreamSynchronize(s), "push count sync")))
+        return rc;
+    const RecKey rk{0, B};
+    if (nD > fineEnd)
+        k_fold_runs<DenseEntry, true, unsigned long long><<<cdiv(nD - fineEnd, 64), 64, 0, s>>>(
+            nD - fineEnd, ~0ull, P<unsigned long long>(h->cdKeysS) + fineEnd, P<int>(h->cdIdsS) + fineEnd,
+            P<float>(h->cdVal), DenseEntry{dense, rk});
+    if (nP > 0) {
+        if ((rc = ensure(h, h->cpKeys, (size_t)nP * 4)) || (rc = ensure(h, h->cpKeysS, (size_t)nP * 4)) ||
+            (rc = ensure(h, h->cpIds, (size_t)nP * 4)) || (rc = ensure(h, h->cpIdsS, (size_t)nP * 4)))
+            return rc;
+        k_push_write<<<cdiv(nA, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), gn, P<int>(h->cpOff),
+                                                   P<unsigned>(h->cpKeys), P<int>(h->cpIds));
+        if ((rc = sort_pairs(h, P<unsigned>(h->cpKeys), P<unsigned>(h->cpKeysS), P<int>(h->cpIds), P<int>(h->cpIdsS),
+                             nP, B, s, "push sort")))
+            return rc;
+        // .cpp:1236-1252: diag(target) += additional[x], x ascending (row-major rows)
+        k_fold_runs<DenseDiag, false, unsigned><<<cdiv(nP, 64), 64, 0, s>>>(
+            nP, 0xffffffffu, P<unsigned>(h->cpKeysS), P<int>(h->cpIdsS), P<float>(h->additional), DenseDiag{dense});
+    }
+    fc = FineContacts{P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
+                      B};
+    return hip_check(h, hipGetLastError(), "contact kernels");
+}
+
 int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s) {
     const int nV = h->nV, L = h->L, tc = h->totalClusters;
     int rc;
@@ -689,24 +861,10 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     float* dense = P<float>(h->dense);
     float* add = P<float>(h->additional);
     const int* gn = P<int>(h->goingNext);
-    // privatize the top level's targets when it is one block (k_collision_hessian)
-    const int topNode = (L > 1 && ceil32(h->levelSize[2 * (L - 1)]) == 32) ? h->levelSize[2 * (L - 1) + 1] : -1;
-    const int gContact =
-        std::max(1, std::min(kContactBlocks, cdiv(h->nStencil, kContactThreads / kLanesPerStencil)));
-    if (h->nStencil) {
-        k_collision_hessian<<<gContact, kContactThreads, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
-                                                                 kContactAdditional, gn, L, topNode, dense, add);
-        for (int l = 1; l < L; ++l)  // child level l: own diagonals (l = 1), then S into level l + 1 (< L)
-            if (l == 1 || l + 1 < L)
-                k_additional_up<<<cdiv(h->levelSize[2 * l], 64), 64, 0, s>>>(h->levelSize[2 * l + 1],
-                                                                             h->levelSize[2 * l], tc, l == 1, gn,
-                                                                             add, dense);
-    }
+    FineContacts fc{};
+    if (h->nStencil && (rc = run_contacts(h, s, fc))) return rc;
     k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
-                                              d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt));
-    if (h->nStencil)
-        k_collision_hessian<<<gContact, kContactThreads, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil,
-                                                                 kContactPairs, gn, L, topNode, dense, add);
+                                              d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt), fc);
     if (L == 1) return hip_check(h, hipGetLastError(), "assembly kernels");
 
     // coarse edge records in (u, k) order
@@ -761,8 +919,9 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                                                                2 * rk.B, s),
                             "record sort")))
             return rc;
-        k_fold_runs<<<cdiv(nRec, 64), 64, 0, s>>>(nRec, rk, P<unsigned long long>(h->recKeysSorted),
-                                                  P<int>(h->recIdsSorted), d_off9, dense);
+        k_fold_runs<DenseEntry, true, unsigned long long><<<cdiv(nRec, 64), 64, 0, s>>>(
+            nRec, (1ull << (2 * rk.B)) - 1, P<unsigned long long>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
+            DenseEntry{dense, rk});
     }
     k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
 

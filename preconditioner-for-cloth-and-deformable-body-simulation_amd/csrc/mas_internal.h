@@ -99,6 +99,10 @@ struct mas_context {
     mas::Buffer dense, inv, slotTable, tileSlot, valuSlot;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
+    // contact records (k_assemble.hip): block entries (d*), additional rows (a*), pushes (p*)
+    mas::Buffer cdCnt, cdOff, cdKeys, cdKeysS, cdIds, cdIdsS, cdVal, cFineOff;
+    mas::Buffer caCnt, caOff, caKeys, caKeysS, caIds, caIdsS, caVal;
+    mas::Buffer cpCnt, cpOff, cpKeys, cpKeysS, cpIds, cpIdsS;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, shardPos1, l1src;
     mas::Buffer chainPrange, chainNeed, chainCnt;  // one-launch coarse chain (k_coarse_chain.hip)
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
@@ -131,7 +135,10 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &tileSlot, &valuSlot, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &termCnt, &termOff, &terms, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &vlist, &voff, &tab, &termCnt, &termOff, &terms,
+                              &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &caCnt, &caOff,
+                              &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
+                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
