@@ -87,13 +87,11 @@ typedef struct {
        measured with HIP events on the apply stream around each kernel group */
     int64_t profiled_applies;
     double apply_ms_avg;       /* apply start -> apply end on the caller stream */
-    double pre_fine_ms_avg;    /* before the fine kernel: coarse chain (serial mode) or fork (overlap mode) */
+    double pre_fine_ms_avg;    /* before the fine kernel: the coarse levels */
     double fine_ms_avg;        /* the fine-level kernel: gather + level-0 block solves (+ prolongation) -- dominant */
-    double post_fine_ms_avg;   /* after it: join with the coarse chain + prolongation pass (overlap mode),
-                                  */
+    double post_fine_ms_avg;   /* after it (0 on the single-GPU path: the prolongation is fused) */
     int64_t apply_mode;        /* coarse levels: 2 = restrictions then all solves, two launches
-                                  (default); 1 = one launch (k_coarse_chain); 0 = one launch per level;
-                                  3 = side-stream overlap */
+                                  (default); 0 = one launch per level */
 } mas_stats;
 
 /* lifecycle */
@@ -136,16 +134,22 @@ int mas_apply_device(mas_handle h, float* d_z4, const float* d_r4, void* stream)
  * major 3x3, ranges[nV+1] == nbr_starts, with the neighbour ids given to
  * mas_allocate), preconditioned by this handle's MAS (precondition = 1) or
  * not at all (precondition = 0, plain CG).  x: initial guess in, solution out.
- * Stops when ||r||_2 <= tol ||b||_2 or after max_iters iterations.  Vectors
- * are [nV][4] fp32 (w written 0); dot products accumulate in fp64 in a fixed
+ * Stops when the returned x satisfies ||b - A x||_2 <= tol ||b||_2 (fp64
+ * evaluation; the fp32 recursive residual only triggers that check, and r is
+ * replaced by b - A x whenever it does) or after max_iters iterations.
+ * Vectors are [nV][4] fp32 (w written 0); the solution accumulates in fp64
+ * and is rounded once at the end; dot products accumulate in fp64 in a fixed
  * order (deterministic).  The reference has no solver: this is the loop its
  * callers run around Preconditioning. */
 typedef struct {
     int iterations;       /* iterations performed */
-    int converged;        /* ||r|| <= tol ||b|| reached */
-    double rel_residual;  /* ||r||_2 / ||b||_2 of the recursively updated residual */
-    double true_rel_residual; /* ||b - A x||_2 / ||b||_2 of the returned x (fp32 vectors: can exceed tol) */
+    int converged;        /* true_rel_residual <= tol */
+    double rel_residual;  /* ||r||_2 / ||b||_2 as last tested (true residual after a replacement) */
+    double true_rel_residual; /* ||b - A x||_2 / ||b||_2 of the returned x, fp64 evaluation */
     double solve_ms;      /* device time from the initial residual to the stop */
+    int first_pass_iterations; /* iterations until the recursive residual first met tol (0: never) --
+                                  what an fp64 PCG would report; the rest drive the fp32 x below tol */
+    int replacements;     /* residual replacements (r = b - A x) performed */
 } mas_pcg_result;
 int mas_pcg_solve_device(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges,
                          float* d_x4, const float* d_b4, int max_iters, float tol, int precondition,

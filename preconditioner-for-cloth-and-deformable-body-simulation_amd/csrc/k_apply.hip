@@ -3,8 +3,7 @@
 // Per apply, on one stream: the coarse levels, then k_solve_fine.  For
 // L >= 3 the coarse levels default to two launches (k_coarse_twopass.hip:
 // all restrictions, then all solves); the per-level form below is kept as
-// coarseMode 0 (and is the L = 2 path), the one-launch chain as mode 1
-// (k_coarse_chain.hip).  All forms are bitwise equal.
+// coarseMode 0 (and is the L = 2 path).  Both forms are bitwise equal.
 //   k_coarse_l1         per level-1 block (one wave): R1 of its 32 nodes from
 //                       r gathered through the Morton map, summed per parent
 //                       in lane order from +0 exactly as the reference's owner
@@ -40,10 +39,15 @@ static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThread
 // than the 256 MiB Infinity Cache), so they are loaded nontemporal: measured
 // 98.8 vs 109.7 us per launch at 1M against default-policy loads (VAR = 0,
 // env MAS_FINE_VARIANT=0 keeps that variant for A/B runs).
-template <int NPROL, int VAR>
+// RZ (the PCG driver's applies, k_pcg.hip): exit at once when *done is set,
+// and emit this workgroup's r.z (fp64; a fixed xor butterfly per wave, then
+// the waves in order) to rzPart[blockIdx.x], so the solver needs no separate
+// pass over r and z.
+template <int NPROL, int VAR, bool RZ>
 __device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, int blk0, int nFineBlk, int nV,
                                                 const float4* __restrict__ r, const int4* __restrict__ vmap,
-                                                const float4* __restrict__ zc, int begin1, float4* __restrict__ z) {
+                                                const float4* __restrict__ zc, int begin1, float4* __restrict__ z,
+                                                double* __restrict__ rzPart) {
     const int lane = threadIdx.x & 63, n = lane & 31;
     const int blk = blk0 + blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
     const bool bvalid = blk < nFineBlk;
@@ -55,30 +59,46 @@ __device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, 
     const float4 rv = r[m.x];
     const float3 rr = vvalid ? make_float3(rv.x, rv.y, rv.z) : make_float3(0.f, 0.f, 0.f);
     float3 out = block_solve(g, tl, rr, lane);
-    if (!vvalid || lane >= 32) return;
-    if (NPROL >= 1) {
-        const float4 a = zc[m.y - begin1];
-        out.x = __fadd_rn(out.x, a.x); out.y = __fadd_rn(out.y, a.y); out.z = __fadd_rn(out.z, a.z);
+    const bool writer = vvalid && lane < 32;
+    if (writer) {
+        if (NPROL >= 1) {
+            const float4 a = zc[m.y - begin1];
+            out.x = __fadd_rn(out.x, a.x); out.y = __fadd_rn(out.y, a.y); out.z = __fadd_rn(out.z, a.z);
+        }
+        if (NPROL >= 2) {
+            const float4 a = zc[m.z - begin1];
+            out.x = __fadd_rn(out.x, a.x); out.y = __fadd_rn(out.y, a.y); out.z = __fadd_rn(out.z, a.z);
+        }
+        if (NPROL >= 3) {
+            const float4 a = zc[m.w - begin1];
+            out.x = __fadd_rn(out.x, a.x); out.y = __fadd_rn(out.y, a.y); out.z = __fadd_rn(out.z, a.z);
+        }
+        z[m.x] = make_float4(out.x, out.y, out.z, 0.f);
     }
-    if (NPROL >= 2) {
-        const float4 a = zc[m.z - begin1];
-        out.x = __fadd_rn(out.x, a.x); out.y = __fadd_rn(out.y, a.y); out.z = __fadd_rn(out.z, a.z);
+    if (RZ) {
+        double a = writer ? (double)out.x * rr.x + (double)out.y * rr.y + (double)out.z * rr.z : 0.0;
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+        __shared__ double sw[kApplyThreads / 64];
+        if (lane == 0) sw[threadIdx.x >> 6] = a;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0.0;
+            for (int w = 0; w < kApplyThreads / 64; ++w) t += sw[w];
+            rzPart[blockIdx.x] = t;
+        }
     }
-    if (NPROL >= 3) {
-        const float4 a = zc[m.w - begin1];
-        out.x = __fadd_rn(out.x, a.x); out.y = __fadd_rn(out.y, a.y); out.z = __fadd_rn(out.z, a.z);
-    }
-    z[m.x] = make_float4(out.x, out.y, out.z, 0.f);
 }
 
 
-template <int NPROL, int VAR>
+template <int NPROL, int VAR, bool RZ>
 __global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __restrict__ inv, int blk0, int nFineBlk,
                                                              int nV, const float4* __restrict__ r,
                                                              const int4* __restrict__ vmap,
                                                              const float4* __restrict__ zc, int begin1,
-                                                             float4* __restrict__ z) {
-    solve_fine_body<NPROL, VAR>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z);
+                                                             float4* __restrict__ z, const int* __restrict__ done,
+                                                             double* __restrict__ rzPart) {
+    if (RZ && *done) return;
+    solve_fine_body<NPROL, VAR, RZ>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, rzPart);
 }
 
 // Coarse levels, one wave per 32-node block; lane n (half 0) owns node
@@ -186,7 +206,9 @@ __device__ __forceinline__ void coarse_block_up(const float4* __restrict__ inv, 
 __global__ __launch_bounds__(kApplyThreads) void k_coarse_l1(const float4* __restrict__ inv, int blkBegin, int nb,
                                                             int count, const int* __restrict__ l1src,
                                                             const float4* __restrict__ r, float4* __restrict__ rc,
-                                                            float4* __restrict__ zc, int begin1) {
+                                                            float4* __restrict__ zc, int begin1,
+                                                            const int* __restrict__ done) {
+    if (done && *done) return;
     const int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
     if (w >= nb) return;  // wave-uniform
     coarse_block_l1(inv, blkBegin + w, blkBegin, count, l1src, r, rc, zc, begin1, threadIdx.x & 63);
@@ -195,7 +217,9 @@ __global__ __launch_bounds__(kApplyThreads) void k_coarse_l1(const float4* __res
 __global__ __launch_bounds__(kApplyThreads) void k_coarse_up(const float4* __restrict__ inv, int blkBegin, int nb,
                                                             int count, const int2* __restrict__ members,
                                                             int childBegin, float4* __restrict__ rc,
-                                                            float4* __restrict__ zc, int begin1) {
+                                                            float4* __restrict__ zc, int begin1,
+                                                            const int* __restrict__ done) {
+    if (done && *done) return;
     const int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
     if (w >= nb) return;  // wave-uniform
     coarse_block_up(inv, blkBegin + w, blkBegin, count, members, childBegin, rc, zc, begin1, threadIdx.x & 63);
@@ -216,13 +240,28 @@ __global__ __launch_bounds__(256) void k_members(int nChild, int childBegin, con
 
 template <int NPROL>
 static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int blk0, int blkEnd, int nV,
-                          const float4* r, const int4* vmap, const float4* zc, int begin1, float4* z) {
-    if (var == 0) k_solve_fine<NPROL, 0><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
-    else k_solve_fine<NPROL, 1><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
+                          const float4* r, const int4* vmap, const float4* zc, int begin1, float4* z,
+                          const int* done, double* rzPart) {
+    if (rzPart) {  // the PCG driver's applies
+        if (var == 0)
+            k_solve_fine<NPROL, 0, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
+                                                                       done, rzPart);
+        else
+            k_solve_fine<NPROL, 1, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
+                                                                       done, rzPart);
+    } else if (var == 0) {
+        k_solve_fine<NPROL, 0, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
+                                                                    nullptr, nullptr);
+    } else {
+        k_solve_fine<NPROL, 1, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
+                                                                    nullptr, nullptr);
+    }
 }
 
 // level-0 blocks [blk0, blkEnd) with prolongation of min(L,4)-1 coarse levels
-void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s) {
+// (rzPart: the PCG hooks, see solve_fine_body)
+void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s,
+                 const int* done, double* rzPart) {
     const int L = h->L;
     const int g = cdiv(blkEnd - blk0, kApplyThreads / 64);
     if (g <= 0) return;
@@ -231,12 +270,14 @@ void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* 
     const float4* zc = P<float4>(h->Zc);
     const int begin1 = h->levelSize[3], nV = h->nV, var = h->fineVariant;
     switch (L < 4 ? L - 1 : 3) {
-        case 0: launch_fine_n<0>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z); break;
-        case 1: launch_fine_n<1>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z); break;
-        case 2: launch_fine_n<2>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z); break;
-        default: launch_fine_n<3>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z); break;
+        case 0: launch_fine_n<0>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart); break;
+        case 1: launch_fine_n<1>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart); break;
+        case 2: launch_fine_n<2>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart); break;
+        default: launch_fine_n<3>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart); break;
     }
 }
+
+int fine_grid(const mas_context* h) { return cdiv(h->nFineBlk, kApplyThreads / 64); }
 
 // coarse levels lFirst..L-1: level 1 from the vertices (k_coarse_l1), then
 // one k_coarse_up launch per level.  (Levels >= 2 in one workgroup separated
@@ -252,10 +293,11 @@ void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStre
         const int nb = ceil32(cnt) / 32;
         if (l == 1)
             k_coarse_l1<<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int>(h->l1src), d_r,
-                                                                      rc, zc, begin1);
+                                                                      rc, zc, begin1, h->applyDone);
         else
             k_coarse_up<<<grid_for_blocks(nb), kApplyThreads, 0, s>>>(inv, beg / 32, nb, cnt, P<int2>(h->members),
-                                                                      h->levelSize[2 * (l - 1) + 1], rc, zc, begin1);
+                                                                      h->levelSize[2 * (l - 1) + 1], rc, zc, begin1,
+                                                                      h->applyDone);
     }
 }
 
@@ -300,36 +342,20 @@ void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float
     const int g = cdiv(blkEnd - blk0, kApplyThreads / 64);
     if (g <= 0) return;
     launch_fine_n<0>(h->fineVariant, g, s, P<float4>(h->inv), blk0, blkEnd, h->nV, r, P<int4>(h->vmap),
-                     P<float4>(h->Zc), h->levelSize[3], z);
+                     P<float4>(h->Zc), h->levelSize[3], z, nullptr, nullptr);
 }
 
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     hipEvent_t* ev = nullptr;
     if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
     if (ev) hipEventRecord(ev[0], s);
-    if (h->L > 1 && h->overlap) {
-        // coarse chain on the side stream, concurrent with the fine blocks;
-        // join, then the prolongation pass (bitwise equal to the fused form)
-        hipEventRecord(h->evFork, s);
-        hipStreamWaitEvent(h->stream2, h->evFork, 0);
-        launch_coarse_levels(h, 1, d_r, h->stream2);
-        hipEventRecord(h->evJoin, h->stream2);
-        if (ev) hipEventRecord(ev[1], s);
-        launch_fine_z0(h, 0, h->nFineBlk, d_r, d_z, s);
-        if (ev) hipEventRecord(ev[2], s);
-        hipStreamWaitEvent(s, h->evJoin, 0);
-        launch_prolong(h, 0, h->nV, d_z, s);
-        if (ev) hipEventRecord(ev[3], s);
-    } else {
-        // coarse levels (mas_internal.h coarseMode); all forms bitwise equal
-        if (h->L > 2 && h->coarseMode == 2) launch_coarse_twopass(h, d_r, s);
-        else if (h->L > 1 && h->coarseMode == 1) launch_coarse_chain(h, d_r, s);
-        else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
-        if (ev) hipEventRecord(ev[1], s);
-        launch_fine(h, 0, h->nFineBlk, d_r, d_z, s);
-        if (ev) hipEventRecord(ev[2], s);
-        if (ev) hipEventRecord(ev[3], s);
-    }
+    // coarse levels (mas_internal.h coarseMode); both forms bitwise equal
+    if (h->L > 2 && h->coarseMode == 2) launch_coarse_twopass(h, d_r, s);
+    else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
+    if (ev) hipEventRecord(ev[1], s);
+    launch_fine(h, 0, h->nFineBlk, d_r, d_z, s, h->applyDone, h->applyRzPart);
+    if (ev) hipEventRecord(ev[2], s);
+    if (ev) hipEventRecord(ev[3], s);
     h->stats.apply_calls++;
     return hip_check(h, hipGetLastError(), "apply kernels");
 }
@@ -356,8 +382,7 @@ int build_l1src(mas_context* h, hipStream_t s) {
     if (rc) return rc;
     k_l1src<<<cdiv((long long)n1Pad * 32, 256), 256, 0, s>>>(n1Pad, n1, P<int2>(h->members), P<int>(h->s2o),
                                                              P<int>(h->l1src));
-    if ((rc = hip_check(h, hipGetLastError(), "l1src"))) return rc;
-    return h->coarseMode == 1 ? build_chain_tables(h, s) : MAS_OK;
+    return hip_check(h, hipGetLastError(), "l1src");
 }
 
 // Apply-side tables, built once per Prepare: members[] for every coarse node,

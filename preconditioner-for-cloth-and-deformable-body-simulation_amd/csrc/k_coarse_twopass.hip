@@ -41,7 +41,8 @@ constexpr int kRestrictWaves = 2;  // waves per workgroup (1 measured 8.4 vs 8.1
 __global__ __launch_bounds__(64 * kRestrictWaves) void k_restrict12(int n1, int begin1, const int* __restrict__ l1src,
                                                     const int* __restrict__ goingNext,
                                                     const int2* __restrict__ members, const float4* __restrict__ r,
-                                                    float4* __restrict__ rc) {
+                                                    float4* __restrict__ rc, const int* __restrict__ done) {
+    if (done && *done) return;
     __shared__ float4 red[kRestrictWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, half = lane >> 5;
     const int c = ((blockIdx.x * kRestrictWaves + wave) * 2 + half) * 32 + j;  // level-1 local id
@@ -103,7 +104,9 @@ struct Solve123 {
 
 __global__ __launch_bounds__(kApplyThreads) void k_solve123(const float4* __restrict__ inv,
                                                            const int2* __restrict__ members, float4* __restrict__ rc,
-                                                           float4* __restrict__ zc, Solve123 q) {
+                                                           float4* __restrict__ zc, Solve123 q,
+                                                           const int* __restrict__ done) {
+    if (done && *done) return;
     const int lane = threadIdx.x & 63, n = lane & 31;
     int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
     if (w >= q.nb1 + q.nb2 + q.nb3) return;  // wave-uniform
@@ -156,15 +159,13 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve123(const float4* __rest
     }
 }
 
-void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
-
 // L >= 3: k_restrict12, k_solve123, and for L = 5 a k_coarse_up for level 4.
 void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
     const int begin1 = h->levelSize[3];
     const int n2 = h->levelSize[4], lv2Begin = h->levelSize[5];
     const int n1 = h->levelSize[2];
     k_restrict12<<<cdiv(n1, 64 * kRestrictWaves), 64 * kRestrictWaves, 0, s>>>(n1, begin1, P<int>(h->l1src), P<int>(h->goingNext),
-                                              P<int2>(h->members), r, P<float4>(h->Rc));
+                                              P<int2>(h->members), r, P<float4>(h->Rc), h->applyDone);
     Solve123 q{};
     q.begin1 = begin1;
     q.lv1Begin = h->levelSize[3];
@@ -182,7 +183,7 @@ void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
         q.nb3 = ceil32(q.n3) / 32;
     }
     k_solve123<<<cdiv(q.nb1 + q.nb2 + q.nb3, kApplyThreads / 64), kApplyThreads, 0, s>>>(
-        P<float4>(h->inv), P<int2>(h->members), P<float4>(h->Rc), P<float4>(h->Zc), q);
+        P<float4>(h->inv), P<int2>(h->members), P<float4>(h->Rc), P<float4>(h->Zc), q, h->applyDone);
     if (h->L >= 5) launch_coarse_levels(h, 4, nullptr, s);
 }
 

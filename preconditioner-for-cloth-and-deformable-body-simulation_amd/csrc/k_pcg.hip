@@ -7,7 +7,22 @@
 //
 //   r = b - A x, z = M r, p = z, rz = r.z
 //   repeat: Ap = A p; alpha = rz / p.Ap; x += alpha p; r -= alpha Ap;
-//           stop when |r| <= tol |b|; z = M r; beta = r.z / rz; p = z + beta p
+//           if |r| <= tol |b|: r = b - A x (residual replacement), stop when
+//           the TRUE |r| <= tol |b|;
+//           z = M r; beta = r.z / rz; p = z + beta p
+//
+// Residual replacement: the fp32 recursion r -= alpha Ap drifts from b - A x
+// (at 1M the recursive residual reached 8.8e-6 while the true one was 5.7e-5),
+// so whenever the recursive test passes, r is recomputed from x and the solve
+// stops only if the true residual passes too; otherwise it continues from the
+// replaced r.  `converged` always refers to the returned x's own residual.
+// The solution accumulates in fp64 (x64, 32 B per vertex) and every true
+// residual is evaluated with fp64 products and sums: an fp32 x updated in
+// place stalls at ~1.1e-5 on the 100x100 grid (alpha p rounds away against
+// x), and an fp32 evaluation of b - A x carries ~1e-5 of cancellation error,
+// while the exact solution rounded to fp32 has 5.9e-6 (fp64 evaluation) --
+// tol = 1e-5 sits right above that floor.  The stop test is taken on the fp32
+// vector the caller receives, round(x64).
 //
 // A is the Prepare input in the caller's vertex order: diag9[nV] and
 // off9[nnz] (3x3 column-major, SeMatrix.h:650-682) with the neighbour CSR
@@ -26,7 +41,14 @@
 // rows are contiguous in the CSR, so one wave-instruction reads ~64
 // consecutive blocks; the G partial products are combined by a fixed xor
 // butterfly; each wave works on 4 row groups at a time so their dependent
-// load chains overlap.  Per iteration: spmv, update_xr, apply (or copy), rz, update_p.
+// load chains overlap.  Per iteration: spmv, update_xr, true (residual
+// replacement, exits at once unless the recursive test passed), the apply (or
+// copy) -- whose fine kernel also emits the r.z partials -- and update_p,
+// which takes the stop decision (iteration count, done flag) and forms p.
+// Every kernel, the apply's included, exits at its first instruction once the
+// solve is done, so the chunks enqueued past convergence cost launches only.
+#include <algorithm>
+
 #include "mas_internal.h"
 
 namespace mas {
@@ -37,11 +59,11 @@ constexpr int kPcgBlocks = 1024;  // fixed grid: partial sums in a fixed order
 struct PcgState {
     double rz[2];  // r.z of the current / next iteration (slot it & 1)
     double rr, bb, alpha, tol2, rrTrue;
-    int done, iters, maxIters, pad;
+    int done, iters, maxIters, firstPass, replacements, pad;
 };
 
-// partial-sum slots (kPcgBlocks doubles each)
-enum { kPartPAp = 0, kPartRR = 1, kPartRZ = 2, kPartBB = 3, kParts = 4 };
+// partial-sum slots; RRX: r.r of the fp32-rounded x64 (the returned vector's residual)
+enum { kPartPAp = 0, kPartRR = 1, kPartRZ = 2, kPartBB = 3, kPartRRX = 4, kParts = 5 };
 
 __device__ __forceinline__ float3 mat3_mul(const float* __restrict__ src, float4 x) {
     // column-major 3x3: y_i = sum_j m[3 j + i] x_j.  The 36-byte block is
@@ -226,13 +248,12 @@ __device__ __forceinline__ void block_partial(double a, double* __restrict__ par
     }
 }
 
-// every workgroup: the same fixed-order sum of the kPcgBlocks partials
-__device__ __forceinline__ double sum_partials(const double* __restrict__ partial) {
+// every workgroup: the same fixed-order sum of n partials (kPcgBlocks by default)
+__device__ __forceinline__ double sum_partials(const double* __restrict__ partial, int n = kPcgBlocks) {
     __shared__ double sa[kPcgThreads];
     __syncthreads();
     double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < kPcgBlocks / kPcgThreads; ++i) t += partial[threadIdx.x + i * kPcgThreads];
+    for (int i = threadIdx.x; i < n; i += kPcgThreads) t += partial[i];
     sa[threadIdx.x] = t;
     __syncthreads();
     for (int s = kPcgThreads / 2; s > 0; s >>= 1) {
@@ -242,8 +263,87 @@ __device__ __forceinline__ double sum_partials(const double* __restrict__ partia
     return sa[0];
 }
 
-// r = b - A x; partials r.r (kPartRR) and b.b (kPartBB).  Also the final
-// true-residual pass (r = scratch).
+// the solution's fp64 accumulator, one per vertex (w unused)
+struct X64 {
+    double x, y, z, w;
+};
+__device__ __forceinline__ void ld3(const float4* __restrict__ p, int v, double (&o)[3]) {
+    const float4 a = p[v];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z;
+}
+__device__ __forceinline__ void ld3(const X64* __restrict__ p, int v, double (&o)[3]) {
+    const double2 a = reinterpret_cast<const double2*>(p + v)[0];
+    o[0] = a.x; o[1] = a.y; o[2] = reinterpret_cast<const double*>(p + v)[2];
+}
+// acc += M x with M a column-major 3x3 of fp32, in fp64; xr: the same with x rounded to fp32
+__device__ __forceinline__ void mat3_mad_d(const float* __restrict__ src, const double (&x)[3], double (&acc)[3],
+                                           double (&accR)[3]) {
+    float m[9];
+    __builtin_memcpy(m, src, 36);
+    double xr[3];
+    for (int j = 0; j < 3; ++j) xr[j] = (double)(float)x[j];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            acc[i] = fma((double)m[3 * j + i], x[j], acc[i]);
+            accR[i] = fma((double)m[3 * j + i], xr[j], accR[i]);
+        }
+}
+
+// The true residual in fp64 over this workgroup's rows (G lanes per row, a
+// fixed xor butterfly): r = fp32(b - A x) is written, rr = |fp32 r|^2,
+// bb = |b|^2, rrx = |b - A round32(x)|^2 (the residual of the fp32 vector
+// the caller gets back).  XV: float4 (an fp32 x) or X64.
+template <int G, class XV>
+__device__ __forceinline__ void residual_rows(int nV, const int* __restrict__ starts, const int* __restrict__ idx,
+                                              const float* __restrict__ diag, const float* __restrict__ off,
+                                              const XV* __restrict__ x, const float4* __restrict__ b,
+                                              float4* __restrict__ r, double& rr, double& bb, double& rrx) {
+    const int lane = threadIdx.x & 63, sub = lane % G;
+    XcdRows xr(nV, 64 / G);
+    rr = 0.0;
+    bb = 0.0;
+    rrx = 0.0;
+    for (int base = xr.first; base < xr.end; base += xr.stride) {
+        const int v = base + lane / G;
+        const bool valid = v < nV;
+        double acc[3] = {0.0, 0.0, 0.0}, accR[3] = {0.0, 0.0, 0.0};
+        if (valid) {
+            double xv[3];
+            if (sub == 0) {
+                ld3(x, v, xv);
+                mat3_mad_d(diag + 9 * (size_t)v, xv, acc, accR);
+            }
+            const int e1 = starts[v + 1];
+            for (int e = starts[v] + sub; e < e1; e += G) {
+                ld3(x, idx[e], xv);
+                mat3_mad_d(off + 9 * (size_t)e, xv, acc, accR);
+            }
+        }
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1)
+            for (int i = 0; i < 3; ++i) {
+                acc[i] += __shfl_xor(acc[i], o);
+                accR[i] += __shfl_xor(accR[i], o);
+            }
+        if (sub == 0 && valid) {
+            const float4 bv = b[v];
+            const double bd[3] = {bv.x, bv.y, bv.z};
+            float rf[3];
+            for (int i = 0; i < 3; ++i) {
+                rf[i] = (float)(bd[i] - acc[i]);
+                rr += (double)rf[i] * rf[i];
+                bb += bd[i] * bd[i];
+                const double e = bd[i] - accR[i];
+                rrx += e * e;
+            }
+            r[v] = make_float4(rf[0], rf[1], rf[2], 0.f);
+        }
+    }
+}
+
+// r = b - A x0 (fp64 evaluation); partials r.r (kPartRR) and b.b (kPartBB);
+// x64 = x0 when given.  Also the final pass over the returned x (r = scratch,
+// x64 null).
 template <int G>
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_residual(int nV, const int* __restrict__ starts,
                                                               const int* __restrict__ idx,
@@ -251,29 +351,42 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_residual(int nV, const int*
                                                               const float* __restrict__ off,
                                                               const float4* __restrict__ x,
                                                               const float4* __restrict__ b, float4* __restrict__ r,
-                                                              double* __restrict__ part) {
-    const int lane = threadIdx.x & 63, sub = lane % G;
-    constexpr int rowsPerWave = kSpmvRows * (64 / G);
-    XcdRows xr(nV, rowsPerWave);
-    double rr = 0.0, bb = 0.0;
-    for (int base = xr.first; base < xr.end; base += xr.stride) {
-        int v[kSpmvRows];
-        float3 ax[kSpmvRows];
-        spmv_rows<G, kSpmvRows>(base, nV, lane, starts, idx, diag, off, x, v, ax);
-#pragma unroll
-        for (int q = 0; q < kSpmvRows; ++q) {
-            if (sub == 0 && v[q] < nV) {
-                const float4 bv = b[v[q]];
-                const float4 rv = make_float4(__fsub_rn(bv.x, ax[q].x), __fsub_rn(bv.y, ax[q].y),
-                                              __fsub_rn(bv.z, ax[q].z), 0.f);
-                r[v[q]] = rv;
-                rr += dot3(make_float3(rv.x, rv.y, rv.z), rv);
-                bb += dot3(make_float3(bv.x, bv.y, bv.z), bv);
-            }
+                                                              X64* __restrict__ x64, double* __restrict__ part) {
+    if (x64)
+        for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
+            const float4 a = x[v];
+            x64[v] = X64{a.x, a.y, a.z, 0.0};
         }
-    }
+    double rr, bb, rrx;
+    residual_rows<G>(nV, starts, idx, diag, off, x, b, r, rr, bb, rrx);
     block_partial(rr, part + kPartRR * kPcgBlocks);
     block_partial(bb, part + kPartBB * kPcgBlocks);
+}
+
+// Residual replacement after update_xr: only when the recursive residual
+// passes the stop test (the same decision in every workgroup), r = b - A x64
+// and the partials of |b - A round32(x64)|^2 (kPartRRX), from which update_p
+// takes the decision.
+template <int G>
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_true(int nV, const int* __restrict__ starts,
+                                                          const int* __restrict__ idx, const float* __restrict__ diag,
+                                                          const float* __restrict__ off, const X64* __restrict__ x64,
+                                                          const float4* __restrict__ b, float4* __restrict__ r,
+                                                          const PcgState* __restrict__ st, double* __restrict__ part) {
+    if (st->done) return;
+    const double rr = sum_partials(part + kPartRR * kPcgBlocks);
+    if (!(rr <= st->tol2 * st->bb)) return;
+    double rt, bb, rrx;
+    residual_rows<G>(nV, starts, idx, diag, off, x64, b, r, rt, bb, rrx);
+    block_partial(rrx, part + kPartRRX * kPcgBlocks);
+}
+
+// the returned solution: x = round32(x64)
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_xout(int nV, const X64* __restrict__ x64, float4* __restrict__ x) {
+    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
+        const X64 a = x64[v];
+        x[v] = make_float4((float)a.x, (float)a.y, (float)a.z, 0.f);
+    }
 }
 
 // 0 iterations done yet: stop at once if |r0| <= tol |b| (or max_iters == 0)
@@ -324,9 +437,9 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __r
     block_partial(pap, part + kPartPAp * kPcgBlocks);
 }
 
-// alpha = rz / p.Ap; x += alpha p; r -= alpha Ap; partials r.r
+// alpha = rz / p.Ap; x64 += alpha p (fp64); r -= alpha Ap (fp32); partials r.r
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_update_xr(int nV, int it, const float4* __restrict__ p,
-                                                               const float4* __restrict__ ap, float4* __restrict__ x,
+                                                               const float4* __restrict__ ap, X64* __restrict__ x,
                                                                float4* __restrict__ r, PcgState* __restrict__ st,
                                                                double* __restrict__ part) {
     if (st->done) return;
@@ -336,9 +449,10 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update_xr(int nV, int it, c
     const float alpha = (float)alphaD;
     double rr = 0.0;
     for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
-        const float4 pv = p[v], av = ap[v], xv = x[v], rv = r[v];
-        x[v] = make_float4(__fmaf_rn(alpha, pv.x, xv.x), __fmaf_rn(alpha, pv.y, xv.y), __fmaf_rn(alpha, pv.z, xv.z),
-                           0.f);
+        const float4 pv = p[v], av = ap[v], rv = r[v];
+        const X64 xv = x[v];
+        x[v] = X64{fma(alphaD, (double)pv.x, xv.x), fma(alphaD, (double)pv.y, xv.y), fma(alphaD, (double)pv.z, xv.z),
+                   0.0};
         const float4 rn = make_float4(__fmaf_rn(-alpha, av.x, rv.x), __fmaf_rn(-alpha, av.y, rv.y),
                                       __fmaf_rn(-alpha, av.z, rv.z), 0.f);
         r[v] = rn;
@@ -347,28 +461,16 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update_xr(int nV, int it, c
     block_partial(rr, part + kPartRR * kPcgBlocks);
 }
 
-// it >= 0: after iteration it, stop if |r| <= tol |b| or it + 1 == max_iters
-// (workgroup 0 records it); otherwise partials r.z.
-// it < 0 (start): partials r.z and p = z.
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_rz(int nV, int it, const float4* __restrict__ r,
+// start: partials r.z and p = z
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_rz(int nV, const float4* __restrict__ r,
                                                         const float4* __restrict__ z, float4* __restrict__ p,
-                                                        PcgState* __restrict__ st, double* __restrict__ part) {
+                                                        const PcgState* __restrict__ st, double* __restrict__ part) {
     if (st->done) return;
-    if (it >= 0) {
-        const double rr = sum_partials(part + kPartRR * kPcgBlocks);
-        const bool stop = (rr <= st->tol2 * st->bb) || it + 1 >= st->maxIters;
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            st->rr = rr;
-            st->iters = it + 1;
-            if (stop) st->done = 1;
-        }
-        if (stop) return;  // the same decision in every workgroup
-    }
     double rz = 0.0;
     for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
         const float4 zv = z[v];
         rz += dot3(make_float3(zv.x, zv.y, zv.z), r[v]);
-        if (it < 0) p[v] = zv;
+        p[v] = zv;
     }
     block_partial(rz, part + kPartRZ * kPcgBlocks);
 }
@@ -380,24 +482,56 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_rz0(PcgState* __restrict__ 
     if (threadIdx.x == 0) st->rz[0] = rz;
 }
 
-// beta = r.z (new) / r.z (old); p = z + beta p; workgroup 0 stores the new r.z
+// After iteration it: the stop decision, then beta = r.z (new) / r.z (old)
+// and p = z + beta p.  The recursive r.r decides whether a replaced residual
+// exists (k_pcg_true ran); if so the returned vector's true r.r is the one
+// tested and recorded.
+// Stop when that passes or it + 1 == max_iters (workgroup 0 records the state;
+// every workgroup takes the same decision).  rzPart: the nRz r.z partials of
+// this iteration's apply (fine kernel workgroups) or copy.
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_update_p(int nV, int it, const float4* __restrict__ z,
                                                               float4* __restrict__ p, PcgState* __restrict__ st,
-                                                              const double* __restrict__ part) {
+                                                              const double* __restrict__ part,
+                                                              const double* __restrict__ rzPart, int nRz) {
     if (st->done) return;
-    const double rzNew = sum_partials(part + kPartRZ * kPcgBlocks);
-    const float beta = (float)(rzNew / st->rz[it & 1]);
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->rz[(it + 1) & 1] = rzNew;
+    double rr = sum_partials(part + kPartRR * kPcgBlocks);
+    const double lim = st->tol2 * st->bb;
+    const bool replaced = rr <= lim;
+    if (replaced) rr = sum_partials(part + kPartRRX * kPcgBlocks);
+    const bool stop = (replaced && rr <= lim) || it + 1 >= st->maxIters;
+    const double rzOld = st->rz[it & 1];
+    const double rzNew = sum_partials(rzPart, nRz);
+    __syncthreads();  // every thread has read st before workgroup 0 writes it
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->rr = rr;
+        st->iters = it + 1;
+        st->rz[(it + 1) & 1] = rzNew;
+        if (replaced) {
+            if (st->firstPass == 0) st->firstPass = it + 1;
+            st->replacements++;
+        }
+        if (stop) st->done = 1;
+    }
+    if (stop) return;
+    const float beta = (float)(rzNew / rzOld);
     for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
         const float4 zv = z[v], pv = p[v];
         p[v] = make_float4(__fmaf_rn(beta, pv.x, zv.x), __fmaf_rn(beta, pv.y, zv.y), __fmaf_rn(beta, pv.z, zv.z), 0.f);
     }
 }
 
+// z = r (no preconditioner) with the r.z partials
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_copy(int nV, const float4* __restrict__ src,
-                                                          float4* __restrict__ dst, const PcgState* __restrict__ st) {
+                                                          float4* __restrict__ dst, const PcgState* __restrict__ st,
+                                                          double* __restrict__ rzPart) {
     if (st->done) return;
-    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) dst[v] = src[v];
+    double rz = 0.0;
+    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
+        const float4 a = src[v];
+        dst[v] = a;
+        rz += dot3(make_float3(a.x, a.y, a.z), a);
+    }
+    if (rzPart) block_partial(rz, rzPart);
 }
 
 template <int G>
@@ -409,6 +543,7 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     float4* z = r + nV;
     float4* p = z + nV;
     float4* ap = p + nV;
+    X64* x64 = reinterpret_cast<X64*>(ap + nV);
     double* part = P<double>(h->pcgPartial);
     const int* idx = P<int>(h->idx);
     const dim3 g(kPcgBlocks), b(kPcgThreads);
@@ -422,37 +557,49 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
         return rc;
     float* ellOff = P<float>(h->pcgEllOff);
     int* ellIdx = P<int>(h->pcgEllIdx);
+    // the apply kernels honour the done flag and the fine kernel emits the
+    // r.z partials while this solve runs (cleared on every return path)
+    const int nRz = precondition ? fine_grid(h) : kPcgBlocks;
+    if ((rc = ensure(h, h->pcgRzPart, (size_t)std::max(nRz, 1) * sizeof(double)))) return rc;
+    double* rzPart = P<double>(h->pcgRzPart);
+    struct Hooks {
+        mas_context* h;
+        ~Hooks() { h->applyDone = nullptr; h->applyRzPart = nullptr; }
+    } hooks{h};
+    h->applyDone = &st->done;
+    h->applyRzPart = rzPart;
     k_pcg_ell<G><<<cdiv(nGroups * 64, 256), 256, 0, s>>>(nV, nGroups, d_ranges, idx, d_off9, ellOff, ellIdx);
-    k_pcg_residual<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, r, part);
+    k_pcg_residual<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, r, x64, part);
     k_pcg_start<<<1, b, 0, s>>>(part, st);
     if (precondition) {
         if ((rc = run_apply(h, z, r, s))) return rc;
     } else {
-        k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st);
+        k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st, nullptr);
     }
-    k_pcg_rz<<<g, b, 0, s>>>(nV, -1, r, z, p, st, part);
+    k_pcg_rz<<<g, b, 0, s>>>(nV, r, z, p, st, part);
     k_pcg_rz0<<<1, b, 0, s>>>(st, part);
     const int chunk = 4;
     for (int it = 0; it < maxIters; it += chunk) {
         for (int k = it; k < it + chunk && k < maxIters; ++k) {
             k_pcg_spmv<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, p, ap, st, part);
-            k_pcg_update_xr<<<g, b, 0, s>>>(nV, k, p, ap, d_x, r, st, part);
+            k_pcg_update_xr<<<g, b, 0, s>>>(nV, k, p, ap, x64, r, st, part);
+            k_pcg_true<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, x64, d_b, r, st, part);
             if (precondition) {
                 if ((rc = run_apply(h, z, r, s))) return rc;
             } else {
-                k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st);
+                k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st, rzPart);
             }
-            k_pcg_rz<<<g, b, 0, s>>>(nV, k, r, z, p, st, part);
-            k_pcg_update_p<<<g, b, 0, s>>>(nV, k, z, p, st, part);
+            k_pcg_update_p<<<g, b, 0, s>>>(nV, k, z, p, st, part, rzPart, nRz);
         }
         if ((rc = hip_check(h, hipMemcpyAsync(&host, st, sizeof(host), hipMemcpyDeviceToHost, s), "D2H pcg state")) ||
             (rc = hip_check(h, hipStreamSynchronize(s), "pcg sync")))
             return rc;
         if (host.done) break;
     }
+    k_pcg_xout<<<g, b, 0, s>>>(nV, x64, d_x);
     hipEventRecord(e1, s);
-    // the true residual of the returned x (the fp32 recursion drifts from it)
-    k_pcg_residual<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, ap, part);
+    // the true residual of the returned x (fp64 evaluation)
+    k_pcg_residual<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, ap, nullptr, part);
     k_pcg_true_finish<<<1, b, 0, s>>>(part, st);
     return MAS_OK;
 }
@@ -461,7 +608,7 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
             const float4* d_b, int maxIters, float tol, int precondition, mas_pcg_result* res, hipStream_t s) {
     const int nV = h->nV;
     int rc;
-    if ((rc = ensure(h, h->pcgVec, (size_t)nV * 16 * 4)) ||
+    if ((rc = ensure(h, h->pcgVec, (size_t)nV * (16 * 4 + sizeof(X64)))) ||
         (rc = ensure(h, h->pcgPartial, (size_t)kPcgBlocks * kParts * sizeof(double))) ||
         (rc = ensure(h, h->pcgState, sizeof(PcgState))))
         return rc;
@@ -491,10 +638,12 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
     hipEventElapsedTime(&ms, e0, e1);
     if (res) {
         res->iterations = host.iters;
-        res->converged = host.rr <= host.tol2 * host.bb;
+        res->converged = host.rrTrue <= host.tol2 * host.bb;  // the returned x's own residual
         res->rel_residual = host.bb > 0 ? sqrt(host.rr / host.bb) : 0.0;
         res->true_rel_residual = host.bb > 0 ? sqrt(host.rrTrue / host.bb) : 0.0;
         res->solve_ms = ms;
+        res->first_pass_iterations = host.firstPass;
+        res->replacements = host.replacements;
     }
     return hip_check(h, hipGetLastError(), "pcg kernels");
 }

@@ -24,10 +24,6 @@
 
 namespace mas {
 
-void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s);
-void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s);
-void launch_prolong(mas_context* h, int v0, int v1, float4* z, hipStream_t s);
-void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
 
 // R1 of the own level-1 segment, one thread per node: the children's
 // original ids come from l1src (32 per node, -1 where none, built at Prepare),

@@ -91,24 +91,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     for (auto& e : h->ev) hipEventCreate(&e);
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
-    if (const char* v = std::getenv("MAS_OVERLAP")) h->overlap = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
-    // Side stream of the MAS_OVERLAP=1 variant (off by default): highest
-    // priority unless MAS_SIDE_PRIORITY=0.  Streams do run kernels
-    // concurrently on MI355X (scripts/dev/stream_overlap.hip), but the level-2
-    // and level-3 kernels, launched once level 1 is done, wait tens of us for
-    // dispatch slots behind the fine kernel's queued workgroups: 148 vs 124
-    // us per apply with either priority, and CU-masked streams were slower
-    // still (profiles/round1/ab/).
-    int prLeast = 0, prGreatest = 0;
-    hipDeviceGetStreamPriorityRange(&prLeast, &prGreatest);
-    if (const char* v = std::getenv("MAS_SIDE_PRIORITY")) prGreatest = std::atoi(v) ? prGreatest : prLeast;
-    if (hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, prGreatest) != hipSuccess ||
-        hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming) != hipSuccess) {
-        mas_destroy(h);
-        return MAS_ERR_HIP;
-    }
     int rc = upload_slot_table(h);
     if (rc != MAS_OK) {
         mas_destroy(h);
@@ -126,8 +109,6 @@ int mas_destroy(mas_handle h) {
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
     for (auto& e : h->prof) hipEventDestroy(e);
-    if (h->evFork) hipEventDestroy(h->evFork);
-    if (h->evJoin) hipEventDestroy(h->evJoin);
     release_comm(h);
     if (h->commStream) {
         hipStreamSynchronize(h->commStream);
@@ -135,10 +116,6 @@ int mas_destroy(mas_handle h) {
     }
     if (h->evRestrict) hipEventDestroy(h->evRestrict);
     if (h->evGathered) hipEventDestroy(h->evGathered);
-    if (h->stream2) {
-        hipStreamSynchronize(h->stream2);
-        hipStreamDestroy(h->stream2);
-    }
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return MAS_OK;
@@ -325,7 +302,7 @@ int mas_get_stats(mas_handle h, mas_stats* out) {
         h->stats.fine_ms_avg = sf / n;
         h->stats.post_fine_ms_avg = sc / n;
     }
-    h->stats.apply_mode = h->overlap ? 3 : h->coarseMode;
+    h->stats.apply_mode = h->coarseMode;
     *out = h->stats;
     return MAS_OK;
 }

@@ -75,13 +75,12 @@ struct mas_context {
     int allocCalls = 0;   // reference m_frameIndex semantics (B-1)
     bool allocated = false, prepared = false, profiling = false;
     bool fromBlob = false;  // restored by mas_load_blob: applies, no Prepare inputs (blob.hip)
-    int overlap = 0;      // 1: coarse chain on stream2 beside the fine blocks (measured slower: 150.8 vs 124.3 us at 1M; env MAS_OVERLAP)
-    hipStream_t stream2 = nullptr;
-    hipEvent_t evFork = nullptr, evJoin = nullptr;
     int factorVariant = 2;  // 2 = register-blocked k_factor_rb; env MAS_FACTOR_VARIANT=0: LDS-row k_factor
     // coarse levels (env MAS_COARSE_MODE): 2 = two launches, restrictions then all
-    // solves (k_coarse_twopass.hip, L >= 3); 1 = one launch climbing by last
-    // arrival (k_coarse_chain.hip; 24.4 vs 22.7 us per level at 1M); 0 = one launch per level
+    // solves (k_coarse_twopass.hip, L >= 3); 0 = one launch per level.  (A
+    // one-launch chain climbing by last arrival, 24.4 vs 22.7 us at 1M, and the
+    // chain on a side stream beside the fine blocks, 150.8 vs 124.3 us, were
+    // measured in round 1 and removed: DESIGN.md section 4.)
     int coarseMode = 2;
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
@@ -104,9 +103,14 @@ struct mas_context {
     mas::Buffer caCnt, caOff, caKeys, caKeysS, caIds, caIdsS, caVal;
     mas::Buffer cpCnt, cpOff, cpKeys, cpKeysS, cpIds, cpIdsS;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, shardPos1, l1src;
-    mas::Buffer chainPrange, chainNeed, chainCnt;  // one-launch coarse chain (k_coarse_chain.hip)
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
+    mas::Buffer pcgRzPart;                               // PCG: r.z partials of the fine apply kernel
+    // set by the PCG driver for the applies of a solve (null otherwise): the
+    // apply kernels exit at once when *applyDone != 0, and the fine kernel
+    // writes one r.z partial per workgroup to applyRzPart
+    const int* applyDone = nullptr;
+    double* applyRzPart = nullptr;
     std::vector<int> l1First;  // first level-1 local id per level-0 bank (+ n1), for sharding
     int shardWorld = 0;
     // one-call sharded apply (mas_shard_apply_device): library-owned segments,
@@ -138,7 +142,7 @@ struct mas_context {
                               &vlist, &voff, &tab, &termCnt, &termOff, &terms,
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
-                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &chainPrange, &chainNeed, &chainCnt, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -172,9 +176,14 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s);
 int upload_slot_table(mas_context* h);
 int prepare_apply_tables(mas_context* h, hipStream_t s);
 int build_l1src(mas_context* h, hipStream_t s);
-int build_chain_tables(mas_context* h, hipStream_t s);
-void launch_coarse_chain(mas_context* h, const float4* r, hipStream_t s);
 void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s);
+void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
+// level-0 blocks [blk0, blkEnd) + prolongation; done / rzPart: PCG hooks (k_apply.hip)
+void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s,
+                 const int* done = nullptr, double* rzPart = nullptr);
+void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s);
+void launch_prolong(mas_context* h, int v0, int v1, float4* z, hipStream_t s);
+int fine_grid(const mas_context* h);  // workgroups of one fine launch over every level-0 block
 int compute_l1_first(mas_context* h, hipStream_t s);
 void release_comm(mas_context* h);  // comm_rccl.hip
 int copy_block_inverse(mas_context* h, int blk, float* out96);

@@ -74,7 +74,8 @@ class mas_shard(ctypes.Structure):
 
 class mas_pcg_result(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int), ("converged", ctypes.c_int), ("rel_residual", ctypes.c_double),
-                ("true_rel_residual", ctypes.c_double), ("solve_ms", ctypes.c_double)]
+                ("true_rel_residual", ctypes.c_double), ("solve_ms", ctypes.c_double),
+                ("first_pass_iterations", ctypes.c_int), ("replacements", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1,14 +1,10 @@
-"""The coarse-level launch forms against one launch per coarse level
-(k_apply.hip): the one-launch chain (k_coarse_chain.hip) and the two-pass form
-(k_coarse_twopass.hip, the default).
+"""The two-pass coarse launch form (k_coarse_twopass.hip, the default)
+against one launch per coarse level (k_apply.hip).
 
-The chain kernel hands coarse residuals/solutions between workgroups inside
-one launch (write-through sc1 stores, agent-scope arrival counters that reset
-themselves; the last arrival at a parent block solves it).  Every sum runs in
-the same order as the per-level form, so the bar is BITWISE equality, per
-apply, over many back-to-back applies with a different residual each time (a
-stale hand-off or a counter not reset would show up as a mismatch in some
-later apply), and the oracle bar (1e-5) for the result itself.
+Every sum runs in the same order in both forms, so the bar is BITWISE
+equality, per apply, over many back-to-back applies with a different residual
+each time (a stale coarse value would show up as a mismatch in some later
+apply), and the oracle bar (1e-5) for the result itself.
 """
 import numpy as np
 import pytest
@@ -19,10 +15,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _handles(mesh, L, contacts, monkeypatch):
-    """Per-level (mode 0), one-launch chain (1), two-pass (2) handles."""
+    """Per-level (mode 0) and two-pass (2) handles."""
     import mas_amd
     hs = []
-    for mode in (0, 1, 2):
+    for mode in (0, 2):
         monkeypatch.setenv("MAS_COARSE_MODE", str(mode))
         hs.append(mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts))
         assert hs[-1].stats()["apply_mode"] == mode
@@ -45,38 +41,38 @@ CASES = [("cloth", 20, 0, 0), ("cloth", 40, 2, 0), ("cloth", 100, 3, 0), ("cloth
 
 
 @pytest.mark.parametrize("kind,W,L,nc", CASES)
-def test_chain_equals_per_level(kind, W, L, nc, monkeypatch):
+def test_twopass_equals_per_level(kind, W, L, nc, monkeypatch):
     import torch
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=11) if nc else None
-    P3, PF, P2 = _handles(mesh, L, contacts, monkeypatch)
+    P3, P2 = _handles(mesh, L, contacts, monkeypatch)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 100 + k)).cuda() for k in range(24)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    for PX in (PF, P2):
+    for PX in (P2,):
         zf = _applies(PX, rs, s)
         for k, (a, b) in enumerate(zip(zf, z3)):
             np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
-        # and again on the same handle (the chain's arrival counters reset themselves)
+        # and again on the same handle
         zf2 = _applies(PX, rs[::-1], s)
         for k, (a, b) in enumerate(zip(zf2, z3[::-1])):
             np.testing.assert_array_equal(a, b, err_msg=f"second pass, apply {k}")
 
 
-def test_chain_1m_contacts_bitwise_and_oracle(monkeypatch):
-    """The bench workload: 1M cloth + 100k VF contacts, 4 levels; chain =
+def test_twopass_1m_contacts_bitwise_and_oracle(monkeypatch):
+    """The bench workload: 1M cloth + 100k VF contacts, 4 levels; two-pass =
     per-level bitwise over 40 back-to-back applies, and the oracle bar."""
     import torch
     from mas_amd import meshgen
     from oracle import Oracle
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    P3, PF, P2 = _handles(mesh, 4, contacts, monkeypatch)
+    P3, P2 = _handles(mesh, 4, contacts, monkeypatch)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 0x5EED + k)).cuda() for k in range(40)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    for PX in (PF, P2):
+    for PX in (P2,):
         zf = _applies(PX, rs, s)
         for k, (a, b) in enumerate(zip(zf, z3)):
             np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
@@ -86,33 +82,3 @@ def test_chain_1m_contacts_bitwise_and_oracle(monkeypatch):
     z_o = o.apply(rs[5].cpu().numpy())
     err = float(np.linalg.norm((zf[5] - z_o)[:, :3]) / np.linalg.norm(z_o[:, :3]))
     assert err <= 1e-5, err
-
-
-def test_chain_interleaved_handles(monkeypatch):
-    """Two handles applied alternately on one stream: each handle's arrival
-    counters are its own."""
-    import torch
-    from mas_amd import meshgen
-    ma, mb = cloth(64), tet(12)
-    import mas_amd
-    monkeypatch.setenv("MAS_COARSE_MODE", "1")
-    A = mas_amd.from_mesh(ma, max_levels=3)
-    B = mas_amd.from_mesh(mb, max_levels=3)
-    monkeypatch.setenv("MAS_COARSE_MODE", "0")
-    A3 = mas_amd.from_mesh(ma, max_levels=3)
-    B3 = mas_amd.from_mesh(mb, max_levels=3)
-    s = torch.cuda.Stream()
-    ra = [torch.from_numpy(meshgen.residual(ma.nV, k)).cuda() for k in range(8)]
-    rb = [torch.from_numpy(meshgen.residual(mb.nV, 50 + k)).cuda() for k in range(8)]
-    za = [torch.zeros_like(r) for r in ra]
-    zb = [torch.zeros_like(r) for r in rb]
-    torch.cuda.synchronize()
-    for k in range(8):
-        A.PreconditioningDevice(za[k], ra[k], s.cuda_stream)
-        B.PreconditioningDevice(zb[k], rb[k], s.cuda_stream)
-    s.synchronize()
-    ea = _applies(A3, ra, s)
-    eb = _applies(B3, rb, s)
-    for k in range(8):
-        np.testing.assert_array_equal(za[k].cpu().numpy(), ea[k])
-        np.testing.assert_array_equal(zb[k].cpu().numpy(), eb[k])

@@ -3,13 +3,20 @@
 Bars:
   * iteration counts within max(3, 5 %) of a float64 numpy PCG driven by the
     CPU oracle's preconditioner on the same right-hand side (the GPU loop runs
-    fp32 vectors with fp64 dot products, so counts may differ by a few);
+    fp32 vectors with fp64 dot products, so counts may differ by a few) --
+    compared at the iteration where the recursive residual first met tol,
+    which is where an fp64 PCG stops; driving the returned fp32 x's own
+    residual below tol (its rounding floor is 5.9e-6 on the 100x100 grid)
+    may take a few more, held to 15 % + 5;
   * the SURVEY §4 known answer: MAS / unpreconditioned iteration ratio on the
     100x100 grid in the reference's band (0.21 at 3 levels, 0.44 at 1 level);
-  * the returned x satisfies ||b - A x|| <= 10 tol ||b|| in float64 (fp32
-    vectors: the recursive residual drifts from the true one; measured 6e-5
-    at tol 1e-5 on the 100x100 grid), and the library's own true-residual
-    report agrees with the float64 one;
+  * the returned x satisfies ||b - A x|| <= tol ||b||: the solver replaces
+    the drifting fp32 recursive residual by b - A x whenever the recursive test
+    passes and stops only on the true one (the float64 recomputation here may
+    differ from the fp32 one in the last digits: 1.1 tol), and the library's
+    own true-residual report agrees with the float64 one;
+  * the apply hooks of a solve (done flag, r.z partials) are gone afterwards:
+    a plain apply after a solve equals one before it;
   * run-to-run bitwise determinism, host and device entry points equal.
 """
 import numpy as np
@@ -48,8 +55,9 @@ def test_pcg_iterations_match_cpu_and_known_answer(W, L, band):
     b = meshgen.residual(mesh.nV, 0x5EED)
     x, res = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=3000, tol=TOL)
     assert res["converged"], res
+    assert res["true_rel_residual"] <= TOL, res
     tr = _true_rel_res(mesh, x, b)
-    assert tr <= 10 * TOL, (tr, res)
+    assert tr <= 1.1 * TOL, (tr, res)
     assert abs(res["true_rel_residual"] - tr) <= 0.05 * tr + 1e-7, (res, tr)
     x0, res0 = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=3000, tol=TOL, precondition=False)
     assert res0["converged"], res0
@@ -67,9 +75,13 @@ def test_pcg_iterations_match_cpu_and_known_answer(W, L, band):
 
     it_cpu = _pcg_iters(A, bv, prec, tol=TOL)
     it_cpu0 = _pcg_iters(A, bv, lambda v: v, tol=TOL)
-    assert abs(res["iterations"] - it_cpu) <= max(3, 0.05 * it_cpu), (res, it_cpu)
-    assert abs(res0["iterations"] - it_cpu0) <= max(3, 0.05 * it_cpu0), (res0, it_cpu0)
-    ratio = res["iterations"] / res0["iterations"]
+    for rs, ic in ((res, it_cpu), (res0, it_cpu0)):
+        first = rs["first_pass_iterations"]
+        assert abs(first - ic) <= max(3, 0.05 * ic), (rs, ic)
+        assert first <= rs["iterations"] <= 1.15 * first + 5, rs
+        assert rs["replacements"] >= 1, rs
+    assert res0["true_rel_residual"] <= TOL, res0
+    ratio = res["first_pass_iterations"] / res0["first_pass_iterations"]
     assert band[0] <= ratio <= band[1], (res, res0, ratio)
 
 
@@ -79,11 +91,13 @@ def test_pcg_deterministic_and_device_path():
     mesh = tet(12)
     P = _setup(mesh, 0)
     b = meshgen.residual(mesh.nV, 3)
+    z_before = P.Preconditioning(None, b)
     x1, r1 = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=500, tol=TOL)
+    np.testing.assert_array_equal(P.Preconditioning(None, b), z_before)
     x2, r2 = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=500, tol=TOL)
     # valence 14: the 16-lane SpMV over the ELL copy of the CSR blocks
     assert r1["converged"], r1
-    assert _true_rel_res(mesh, x1, b) <= 10 * TOL
+    assert _true_rel_res(mesh, x1, b) <= 1.1 * TOL
     np.testing.assert_array_equal(x1, x2)
     assert r1["iterations"] == r2["iterations"]
     dd = torch.from_numpy(np.ascontiguousarray(mesh.diag, np.float32)).cuda()
