@@ -261,6 +261,10 @@ int mas_get_neighbors(mas_handle h, int* nbr_num, int* nbr);
  * and its inverse unpacked to 96x96. */
 int mas_get_block_matrix(mas_handle h, int blk, float* out96x96);
 int mas_get_block_inverse(mas_handle h, int blk, float* out96x96);
+/* The residual hierarchy of the most recent single-GPU apply
+ * (BuildResidualHierarchy .cpp:1548-1598): R of every coarse node, ids
+ * begin_1 .. total_clusters-1, as out4[total_clusters - begin_1][4]. */
+int mas_get_coarse_residual(mas_handle h, float* out4);
 
 #ifdef __cplusplus
 }

@@ -942,6 +942,7 @@ const int* orc_nbr_num(const orc_state* s) { return s->nbrNum; }
 const int* orc_nbr(const orc_state* s) { return s->nbr; }
 const int* orc_coarse_space_tables(const orc_state* s) { return s->cst; }
 const int* orc_going_next(const orc_state* s) { return s->goingNext; }
+const float* orc_mapped_r(const orc_state* s) { return s->mappedR; }
 const int* orc_coarse_tables(const orc_state* s) { return s->coarseTables; }
 const unsigned* orc_fine_connect_mask(const orc_state* s) { return s->fineMask; }
 const int* orc_stencil_index_mapped(const orc_state* s) { return s->stencilIdx; }

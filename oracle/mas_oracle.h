@@ -83,6 +83,7 @@ const int* orc_stencil_index_mapped(const orc_state* s); /* [nStencil][5] */
 int orc_block_matrix(const orc_state* s, int blk, float* A96);
 int orc_block_inverse(const orc_state* s, int blk, float* inv96);
 const float* orc_inv_packed(const orc_state* s);  /* [nBlk][4704] reference packing */
+const float* orc_mapped_r(const orc_state* s);    /* m_mappedR [capacity][4] after orc_apply */
 
 /* The reference's Morton encode of one normalised point (SeMorton.h:75-86). */
 uint64_t orc_morton_encode(float x, float y, float z);

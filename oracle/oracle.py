@@ -46,7 +46,7 @@ def lib():
         L.orc_aabb.argtypes = [_P, _P, _P]
         for name in ("orc_morton", "orc_s2o", "orc_o2s", "orc_nbr_num", "orc_nbr", "orc_coarse_space_tables",
                      "orc_going_next", "orc_coarse_tables", "orc_fine_connect_mask", "orc_inv_packed",
-                     "orc_stencil_index_mapped"):
+                     "orc_stencil_index_mapped", "orc_mapped_r"):
             getattr(L, name).argtypes = [_P]
             getattr(L, name).restype = _P
         L.orc_block_matrix.argtypes = [_P, _I, _P]
@@ -152,6 +152,10 @@ class Oracle:
             fine_connect_mask=_view(self._L.orc_fine_connect_mask(self.h), np.uint32, nV),
             level_size=self.level_size(),
         )
+
+    def mapped_r(self):
+        """m_mappedR after the last apply: [total_clusters, 4] (the residual hierarchy)."""
+        return _view(self._L.orc_mapped_r(self.h), np.float32, 4 * self.total_clusters).reshape(-1, 4).copy()
 
     def block_matrix(self, blk):
         A = np.zeros((96, 96), dtype=np.float32)

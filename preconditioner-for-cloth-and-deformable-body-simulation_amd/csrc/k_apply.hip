@@ -1,18 +1,17 @@
 // k_apply.hip -- Preconditioning (.cpp:100-110, 1548-1719): the hot path.
 //
 // Per apply, on one stream: the coarse levels, then k_solve_fine.  For
-// L >= 3 the coarse levels default to two launches (k_coarse_twopass.hip:
-// all restrictions, then all solves); the per-level form below is kept as
+// L >= 3 the coarse levels default to two launches (k_coarse.hip: the
+// restrictions, then every solve); the per-level form below is kept as
 // coarseMode 0 (and is the L = 2 path).  Both forms are bitwise equal.
 //   k_coarse_l1         per level-1 block (one wave): R1 of its 32 nodes from
 //                       r gathered through the Morton map, summed per parent
 //                       in lane order from +0 exactly as the reference's owner
 //                       loop (BuildResidualHierarchy .cpp:1558-1574); then
 //                       Z1 = Inv_b R1 (SchwarzLocalXSym .cpp:1600-1696).
-//   k_coarse_up         l = 2..L-1, one launch per level: R_l from
-//                       R_{l-1} the same way (level 2 is the reference's
-//                       level-1-id-order sum, .cpp:1581-1590; level >= 3 sums
-//                       R_{l-1}, same value up to fp association), then Z_l.
+//   k_coarse_up         level 2: R2 from R1 the same way (the reference's
+//                       level-1-id-order sum, .cpp:1581-1590), then Z2;
+//                       levels >= 3: k_coarse_deep (k_coarse.hip).
 //   k_solve_fine        every level-0 block fused with the gather r[s2o[v]]
 //                       and the prolongation z[s2o[v]] = Z0 + Z1[a1] + Z2[a2]
 //                       + Z3[a3] (CollectFinalZ .cpp:1698-1719, min(L,4)-1
@@ -107,9 +106,8 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __re
 // .cpp:590-625 / 917-954).  Every child value is gathered up front (one
 // latency), then lane n adds its children in lane order from +0 -- the
 // reference's accumulation order for level 1 (.cpp:1560-1572) and level 2
-// (level-1 id order, .cpp:1581-1590); level >= 3 sums R_{l-1} (the reference
-// sums R_1 directly: same value up to fp association).  Then
-// Z_l = Inv_b R_l; R_l and Z_l are stored.
+// (level-1 id order, .cpp:1581-1590).  Then Z_l = Inv_b R_l; R_l and Z_l are
+// stored.
 //
 // Level 1 reads its children's original vertex ids from l1src (32 ids per
 // level-1 node, -1 where the lane is not a child; built at Prepare), so the
@@ -279,16 +277,18 @@ void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* 
 
 int fine_grid(const mas_context* h) { return cdiv(h->nFineBlk, kApplyThreads / 64); }
 
-// coarse levels lFirst..L-1: level 1 from the vertices (k_coarse_l1), then
-// one k_coarse_up launch per level.  (Levels >= 2 in one workgroup separated
-// by barriers measured 99 us at 1M: a 1024-thread workgroup caps the block
-// solve at 128 VGPRs and it spills; fewer waves serialise the blocks.)
+// coarse levels lFirst..L-1: level 1 from the vertices (k_coarse_l1), level
+// 2 from R1 (k_coarse_up), levels >= 3 in one k_coarse_deep launch (R folded
+// from R1 in the reference's order, k_coarse.hip).  (Levels >= 2 in
+// one workgroup separated by barriers measured 99 us at 1M: a 1024-thread
+// workgroup caps the block solve at 128 VGPRs and it spills; fewer waves
+// serialise the blocks.)
 void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s) {
     const float4* inv = P<float4>(h->inv);
     float4* rc = P<float4>(h->Rc);
     float4* zc = P<float4>(h->Zc);
     const int begin1 = h->levelSize[3];
-    for (int l = lFirst; l < h->L; ++l) {
+    for (int l = lFirst; l < h->L && l < 3; ++l) {
         const int cnt = h->levelSize[2 * l], beg = h->levelSize[2 * l + 1];
         const int nb = ceil32(cnt) / 32;
         if (l == 1)
@@ -299,6 +299,7 @@ void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStre
                                                                       h->levelSize[2 * (l - 1) + 1], rc, zc, begin1,
                                                                       h->applyDone);
     }
+    if (h->L >= 4) launch_coarse_deep(h, nullptr, nullptr, s);
 }
 
 // z[s2o[v]] += Z1[a1]; += Z2[a2]; += Z3[a3] for v in [v0, v1) -- the
@@ -346,6 +347,7 @@ void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float
 }
 
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
+    if (h->L >= 4 && !h->deepOff.p) return fail(h, MAS_ERR_STATE, "apply: deep-level lists not built");
     hipEvent_t* ev = nullptr;
     if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
     if (ev) hipEventRecord(ev[0], s);
@@ -382,11 +384,13 @@ int build_l1src(mas_context* h, hipStream_t s) {
     if (rc) return rc;
     k_l1src<<<cdiv((long long)n1Pad * 32, 256), 256, 0, s>>>(n1Pad, n1, P<int2>(h->members), P<int>(h->s2o),
                                                              P<int>(h->l1src));
-    return hip_check(h, hipGetLastError(), "l1src");
+    if ((rc = hip_check(h, hipGetLastError(), "l1src"))) return rc;
+    return build_deep_lists(h, s);  // level 3 (L >= 4)
 }
 
-// Apply-side tables, built once per Prepare: members[] for every coarse node,
-// l1src for level 1.
+// Apply-side tables, built once per Prepare (and by mas_load_blob from the
+// restored maps): members[] for every coarse node, l1src for level 1, the
+// deep-level descendant lists.
 int prepare_apply_tables(mas_context* h, hipStream_t s) {
     const int nV = h->nV, L = h->L;
     const int begin1 = h->levelSize[3];

@@ -759,6 +759,11 @@ static int sort_pairs(mas_context* h, const K* kin, K* kout, const int* vin, int
                      what);
 }
 
+int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
+                   hipStream_t s, const char* what) {
+    return sort_pairs(h, kin, kout, vin, vout, n, bits, s, what);
+}
+
 // The contact part of the assembly in the reference's single-thread order
 // (see "contacts" above): on return the coarse blocks hold the contact block
 // entries and the additional pushes, `additional` holds every node's contact

@@ -9,7 +9,8 @@
 //   k_shard_coarse12 own level-1 blocks (Z1 = Inv R1) and every level-2 block
 //                    (R2 from the gathered R1, Z2), straight from the
 //                    gathered segments, one launch
-//   k_coarse_up      every block of levels >= 3 (tiny, redundant on all ranks)
+//   k_coarse_deep    every block of levels >= 3 (R folded from the gathered
+//                    R1 in the reference's order; redundant on all ranks)
 //   k_solve_fine     own level-0 blocks + prolongation, z of own vertices
 // or, overlapped (mas_apply_shard_fine / _complete): k_solve_fine without the
 // coarse terms while the allgather is in flight, then the coarse kernels and
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(256) void k_shard_pos1(int n1, int world, int segMa
 // blocks (Z1 = Inv R1), waves [nOwn1, nOwn1 + nb2) compute R2 of every level-2
 // block -- each node sums its children's R1 in child-lane order from +0, as
 // k_coarse_up -- and solve it.  Both only read the gathered R1, so they are
-// independent; levels >= 3 follow as k_coarse_up launches.  Replaces unpack +
+// independent; levels >= 3 follow as one k_coarse_deep launch.  Replaces unpack +
 // own level-1 solve + level-2 launch (three latency-bound launches).
 __global__ __launch_bounds__(kApplyThreads) void k_shard_coarse12(
     const float4* __restrict__ inv, const float4* __restrict__ gathered, const int* __restrict__ pos1, int own1Blk0,
@@ -216,6 +217,7 @@ int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r
 // levels >= 2.
 static int shard_coarse(mas_context* h, const mas_shard& sh, int world, const float* d_gathered4, hipStream_t s) {
     int rc;
+    if (h->L >= 4 && !h->deepOff.p) return fail(h, MAS_ERR_STATE, "shard apply: deep-level lists not built");
     const int n1 = h->levelSize[2];
     if (h->shardWorld != world) {  // per-rank segment offsets (level-1 local ids) -> pos1
         std::vector<int> off(world + 1);
@@ -227,6 +229,7 @@ static int shard_coarse(mas_context* h, const mas_shard& sh, int world, const fl
             (rc = hip_check(h, hipMemsetAsync(h->shardPos1.p, 0, (size_t)ceil32(n1) * 4, s), "memset pos1")))
             return rc;
         k_shard_pos1<<<cdiv(n1, 256), 256, 0, s>>>(n1, world, sh.seg_max, P<int>(h->shardOff), P<int>(h->shardPos1));
+        if ((rc = build_deep_shard_idx(h, s))) return rc;
         h->shardWorld = world;
     }
     const int begin1 = h->levelSize[3];
@@ -239,7 +242,8 @@ static int shard_coarse(mas_context* h, const mas_shard& sh, int world, const fl
         k_shard_coarse12<<<cdiv(nOwn1 + nb2, kApplyThreads / 64), kApplyThreads, 0, s>>>(
             P<float4>(h->inv), reinterpret_cast<const float4*>(d_gathered4), P<int>(h->shardPos1), begin1 / 32 + own0,
             nOwn1, n1, lv2Blk0, nb2, n2, P<int2>(h->members), begin1, P<float4>(h->Rc), P<float4>(h->Zc));
-    launch_coarse_levels(h, 3, nullptr, s);
+    // levels >= 3: R folded from the gathered R1 in the reference's order
+    launch_coarse_deep(h, reinterpret_cast<const float4*>(d_gathered4), P<int>(h->deepIdxShard), s);
     return MAS_OK;
 }
 

@@ -370,4 +370,14 @@ int mas_get_block_inverse(mas_handle h, int blk, float* out96) {
     return copy_block_inverse(h, blk, out96);
 }
 
+int mas_get_coarse_residual(mas_handle h, float* out4) {
+    if (!h || !out4) return MAS_ERR_ARG;
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "coarse residual before prepare");
+    const int nCoarse = h->totalClusters - h->levelSize[3];
+    if (nCoarse <= 0) return MAS_OK;
+    hipSetDevice(h->device);
+    hipDeviceSynchronize();  // the apply may have run on any stream
+    return hip_check(h, hipMemcpy(out4, h->Rc.p, (size_t)nCoarse * 16, hipMemcpyDeviceToHost), "D2H Rc");
+}
+
 }  // extern "C"

@@ -39,6 +39,17 @@ struct DevStencil {
     float dir[3];
 };
 
+// Level 3 (k_coarse.hip): node T's R is folded from R1 over T's
+// level-1 descendants in id order, list slots T * stride .. + stride (zero /
+// -1 padded); idx[slot] is a position in src (Rc, or the gathered segments of
+// a sharded apply), or src is already in list order (deepR1, idx null).
+struct DeepArgs {
+    const int* idx;
+    const float4* src;
+    int lv3Begin, stride;
+    int* cnt;           // per level-3 block: node arrivals (the last one solves the block)
+};
+
 struct Buffer {
     void* p = nullptr;
     size_t bytes = 0;
@@ -76,11 +87,10 @@ struct mas_context {
     bool allocated = false, prepared = false, profiling = false;
     bool fromBlob = false;  // restored by mas_load_blob: applies, no Prepare inputs (blob.hip)
     int factorVariant = 2;  // 2 = register-blocked k_factor_rb; env MAS_FACTOR_VARIANT=0: LDS-row k_factor
-    // coarse levels (env MAS_COARSE_MODE): 2 = two launches, restrictions then all
-    // solves (k_coarse_twopass.hip, L >= 3); 0 = one launch per level.  (A
-    // one-launch chain climbing by last arrival, 24.4 vs 22.7 us at 1M, and the
-    // chain on a side stream beside the fine blocks, 150.8 vs 124.3 us, were
-    // measured in round 1 and removed: DESIGN.md section 4.)
+    // coarse levels (env MAS_COARSE_MODE): 2 = two launches, restrictions then
+    // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (One-launch
+    // forms and the side-stream overlap were measured slower: DESIGN.md
+    // section 4.)
     int coarseMode = 2;
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
@@ -103,6 +113,11 @@ struct mas_context {
     mas::Buffer caCnt, caOff, caKeys, caKeysS, caIds, caIdsS, caVal;
     mas::Buffer cpCnt, cpOff, cpKeys, cpKeysS, cpIds, cpIdsS;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, shardPos1, l1src;
+    // level-3 descendant lists (k_coarse.hip): sort scratch, list
+    // offsets, deepIdx = level-1 id per list slot, deepPos = list slot of
+    // every level-1 node, R1 in list order (deepR1), per-block arrival counters
+    mas::Buffer deepKeys, deepVals, deepIdx, deepOff, deepPos, deepR1, deepCnt, deepIdxShard;
+    int deepStride = 0;  // list slots per level-3 node (the longest list, rounded up to 4)
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
     mas::Buffer pcgRzPart;                               // PCG: r.z partials of the fine apply kernel
@@ -142,7 +157,7 @@ struct mas_context {
                               &vlist, &voff, &tab, &termCnt, &termOff, &terms,
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
-                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -178,6 +193,11 @@ int prepare_apply_tables(mas_context* h, hipStream_t s);
 int build_l1src(mas_context* h, hipStream_t s);
 void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s);
 void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
+void launch_coarse_deep(mas_context* h, const float4* src, const int* idx, hipStream_t s);
+int build_deep_lists(mas_context* h, hipStream_t s);
+int build_deep_shard_idx(mas_context* h, hipStream_t s);
+int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
+                   hipStream_t s, const char* what);
 // level-0 blocks [blk0, blkEnd) + prolongation; done / rzPart: PCG hooks (k_apply.hip)
 void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s,
                  const int* done = nullptr, double* rzPart = nullptr);

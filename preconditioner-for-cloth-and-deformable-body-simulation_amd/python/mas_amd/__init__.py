@@ -21,7 +21,7 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libmas_amd.so")
+LIB_PATH = os.path.join(LIB_DIR, os.environ.get("MAS_LIB_NAME", "libmas_amd.so"))  # dev: the probe build
 FACADE_PATH = os.path.join(LIB_DIR, "libSeSchwarzPreconditioner.so")
 
 MAS_OK = 0
@@ -36,6 +36,7 @@ ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_allocate", "mas_prepare",
            "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_get_info",
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
+           "mas_get_coarse_residual",
            "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
            "mas_apply_shard_fine", "mas_apply_shard_complete", "mas_shard_apply_device", "mas_rccl_unique_id",
            "mas_rccl_init", "mas_shard_apply_rccl",
@@ -120,6 +121,7 @@ def lib():
         L.mas_get_neighbors.argtypes = [P, P, P]
         L.mas_get_block_matrix.argtypes = [P, I, P]
         L.mas_get_block_inverse.argtypes = [P, I, P]
+        L.mas_get_coarse_residual.argtypes = [P, P]
         L.mas_shard_plan.argtypes = [I, P, I, I, ctypes.POINTER(mas_shard)]
         L.mas_shard_setup.argtypes = [P, I, I, ctypes.POINTER(mas_shard)]
         L.mas_apply_shard_restrict.argtypes = [P, I, I, P, P, P]
@@ -463,6 +465,16 @@ class SeSchwarzPreconditioner:
         B = np.zeros((96, 96), np.float32)
         self._check(self._L.mas_get_block_inverse(self.h, blk, _ptr(B)), "get_block_inverse")
         return B
+
+    def coarse_residual(self):
+        """R of every coarse node (ids begin_1 .. total_clusters-1) after the last apply, [n, 4] float32."""
+        info = self.info()
+        begin1 = int(info["level_size"].reshape(-1)[3])
+        n = info["total_clusters"] - begin1
+        R = np.zeros((max(n, 0), 4), np.float32)
+        if n > 0:
+            self._check(self._L.mas_get_coarse_residual(self.h, _ptr(R)), "get_coarse_residual")
+        return R
 
 
 def from_mesh(mesh, max_levels=0, contacts=None, **kw) -> SeSchwarzPreconditioner:

@@ -1,0 +1,83 @@
+"""The residual hierarchy (BuildResidualHierarchy, .cpp:1548-1598) bitwise
+against the oracle, at every coarse level.
+
+The reference sums level 1 in lane order and every level >= 2 by walking the
+level-1 ids in order and adding each level-1 R into all its ancestors
+(.cpp:1577-1590), so a level-l R (l >= 3) is a left fold of R1 values -- not
+a sum of the level-(l-1) R.  The GPU follows that order (k_restrict12 for
+levels 1-2, the deep folds of k_coarse_twopass.hip for levels >= 3), so R of
+every real coarse node of the prolonged levels (1..3; level 4 never reaches
+z, B-6, and is not computed) equals the oracle's m_mappedR bit for bit, in
+both coarse launch forms.
+"""
+import numpy as np
+import pytest
+
+from conftest import cloth, tet
+
+pytestmark = pytest.mark.gpu
+
+
+def _real_nodes(ls, L):
+    """(begin, count) of coarse levels 1..min(L - 1, 3) from the reference level
+    table: level 4 (L = 5) is never prolonged (CollectFinalZ, B-6), so the
+    library does not compute it."""
+    flat = ls.reshape(-1)
+    return [(int(flat[2 * l + 1]), int(flat[2 * l])) for l in range(1, min(L, 4))]
+
+
+def _check(P, o, r, tag=""):
+    import torch
+    rd = torch.from_numpy(r).cuda()
+    zd = torch.zeros_like(rd)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    P.PreconditioningDevice(zd, rd, s.cuda_stream)
+    s.synchronize()
+    Rg = P.coarse_residual()
+    o.apply(r)
+    Ro = o.mapped_r()
+    info = P.info()
+    ls, L = info["level_size"], info["num_levels"]
+    begin1 = int(ls.reshape(-1)[3])
+    for lv, (b, n) in enumerate(_real_nodes(ls, L), start=1):
+        g = Rg[b - begin1:b - begin1 + n, :3]
+        e = Ro[b:b + n, :3]
+        bad = np.flatnonzero(np.any(g.view(np.uint32) != e.view(np.uint32), axis=1))
+        assert bad.size == 0, (tag, lv, n, bad[:5], g[bad[:3]], e[bad[:3]])
+
+
+@pytest.mark.parametrize("kind,W,L,nc", [("cloth", 100, 4, 0), ("cloth", 256, 4, 2000), ("cloth", 512, 5, 0),
+                                         ("tet", 16, 4, 0), ("cloth", 64, 3, 0)])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_residual_hierarchy_bitwise(kind, W, L, nc, mode, monkeypatch):
+    import mas_amd
+    from mas_amd import meshgen
+    from oracle import Oracle
+    monkeypatch.setenv("MAS_COARSE_MODE", str(mode))
+    mesh = cloth(W) if kind == "cloth" else tet(W)
+    contacts = meshgen.vf_contacts(mesh, nc, seed=5) if nc else None
+    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
+    o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], L, 8)
+    o.allocate(mesh)
+    if contacts is not None:
+        o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
+    else:
+        o.prepare(mesh)
+    for k in range(3):
+        _check(P, o, meshgen.residual(mesh.nV, 40 + k), f"apply {k}")
+
+
+def test_residual_hierarchy_1m_contacts():
+    """The bench workload (1M cloth + 100k VF contacts, 4 levels): the level-3
+    nodes each fold ~1 000 level-1 values."""
+    import mas_amd
+    from mas_amd import meshgen
+    from oracle import Oracle
+    mesh = cloth(1024)
+    contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
+    P = mas_amd.from_mesh(mesh, max_levels=4, contacts=contacts)
+    o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], 4, 8)
+    o.allocate(mesh)
+    o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
+    _check(P, o, meshgen.residual(mesh.nV, 0x5EED))
