@@ -9,8 +9,9 @@
 //   k_shard_coarse12 own level-1 blocks (Z1 = Inv R1) and every level-2 block
 //                    (R2 from the gathered R1, Z2), straight from the
 //                    gathered segments, one launch
-//   k_coarse_deep    every block of levels >= 3 (R folded from the gathered
-//                    R1 in the reference's order; redundant on all ranks)
+//                    and, in the same launch, every level-3 node (R folded
+//                    from the gathered R1 in the reference's order; redundant
+//                    on all ranks)
 //   k_solve_fine     own level-0 blocks + prolongation, z of own vertices
 // or, overlapped (mas_apply_shard_fine / _complete): k_solve_fine without the
 // coarse terms while the allgather is in flight, then the coarse kernels and
@@ -22,6 +23,7 @@
 #include <vector>
 
 #include "block_solve.h"
+#include "deep_fold.h"
 
 namespace mas {
 
@@ -86,14 +88,20 @@ __global__ __launch_bounds__(256) void k_shard_pos1(int n1, int world, int segMa
 // blocks (Z1 = Inv R1), waves [nOwn1, nOwn1 + nb2) compute R2 of every level-2
 // block -- each node sums its children's R1 in child-lane order from +0, as
 // k_coarse_up -- and solve it.  Both only read the gathered R1, so they are
-// independent; levels >= 3 follow as one k_coarse_deep launch.  Replaces unpack +
-// own level-1 solve + level-2 launch (three latency-bound launches).
+// independent.  The first nDeep workgroups fold level 3 (every node, from the
+// gathered R1 through deepIdxShard, in the reference's order: deep_fold.h)
+// in the same launch.  Replaces unpack + own level-1 solve + one launch per
+// coarser level (latency-bound launches).
 __global__ __launch_bounds__(kApplyThreads) void k_shard_coarse12(
     const float4* __restrict__ inv, const float4* __restrict__ gathered, const int* __restrict__ pos1, int own1Blk0,
     int nOwn1, int n1, int lv2Blk0, int nb2, int n2, const int2* __restrict__ members, int begin1,
-    float4* __restrict__ rc, float4* __restrict__ zc) {
+    float4* __restrict__ rc, float4* __restrict__ zc, DeepArgs d, int nDeep) {
+    if ((int)blockIdx.x < nDeep) {  // workgroup-uniform
+        deep_node<true>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, begin1);
+        return;
+    }
     const int lane = threadIdx.x & 63, n = lane & 31;
-    const int w = blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
+    const int w = (blockIdx.x - nDeep) * (kApplyThreads / 64) + (threadIdx.x >> 6);
     if (w >= nOwn1 + nb2) return;  // wave-uniform
     const bool l1 = w < nOwn1;
     const int blk = l1 ? own1Blk0 + w : lv2Blk0 + (w - nOwn1);
@@ -238,12 +246,13 @@ static int shard_coarse(mas_context* h, const mas_shard& sh, int world, const fl
     const int nb2 = h->L > 2 ? ceil32(h->levelSize[4]) / 32 : 0;
     const int n2 = h->L > 2 ? h->levelSize[4] : 0;
     const int lv2Blk0 = h->L > 2 ? h->levelSize[5] / 32 : 0;
-    if (nOwn1 + nb2 > 0)
-        k_shard_coarse12<<<cdiv(nOwn1 + nb2, kApplyThreads / 64), kApplyThreads, 0, s>>>(
+    // level 3 in the same launch: R folded from the gathered R1 in the reference's order
+    const DeepArgs d = deep_args(h, reinterpret_cast<const float4*>(d_gathered4), P<int>(h->deepIdxShard));
+    const int nDeep = deep_nodes(h);
+    if (nDeep + nOwn1 + nb2 > 0)
+        k_shard_coarse12<<<nDeep + cdiv(nOwn1 + nb2, kApplyThreads / 64), kApplyThreads, 0, s>>>(
             P<float4>(h->inv), reinterpret_cast<const float4*>(d_gathered4), P<int>(h->shardPos1), begin1 / 32 + own0,
-            nOwn1, n1, lv2Blk0, nb2, n2, P<int2>(h->members), begin1, P<float4>(h->Rc), P<float4>(h->Zc));
-    // levels >= 3: R folded from the gathered R1 in the reference's order
-    launch_coarse_deep(h, reinterpret_cast<const float4*>(d_gathered4), P<int>(h->deepIdxShard), s);
+            nOwn1, n1, lv2Blk0, nb2, n2, P<int2>(h->members), begin1, P<float4>(h->Rc), P<float4>(h->Zc), d, nDeep);
     return MAS_OK;
 }
 

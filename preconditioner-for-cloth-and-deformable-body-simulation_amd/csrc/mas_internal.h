@@ -194,6 +194,8 @@ int build_l1src(mas_context* h, hipStream_t s);
 void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s);
 void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
 void launch_coarse_deep(mas_context* h, const float4* src, const int* idx, hipStream_t s);
+int deep_nodes(const mas_context* h);  // level-3 node ids incl. padding (0 below L = 4)
+mas::DeepArgs deep_args(mas_context* h, const float4* src, const int* idx);
 int build_deep_lists(mas_context* h, hipStream_t s);
 int build_deep_shard_idx(mas_context* h, hipStream_t s);
 int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
