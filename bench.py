@@ -130,6 +130,9 @@ def cpu_baseline(mesh, cfg, contacts, r_np, steps):
                       f"ms/apply {med * 1e3:.2f}"}, z
 
 
+PREP_KEYS = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -182,7 +185,10 @@ def main():
     cfg = dict(cfg, name=args.config)
     contacts = meshgen.vf_contacts(mesh, cfg["contacts"], seed=3) if cfg["contacts"] else None
     t0 = time.perf_counter()
-    P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts, device=local)
+    # sharded path: each rank's Prepare assembles and factors only its own
+    # level-0 blocks (mas_set_prepare_shard); the coarse levels are replicated
+    P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts, device=local,
+                          shard=(rank, world) if sharded_path else None)
     setup_s = time.perf_counter() - t0
     info = P.info()
     st_first = P.stats()
@@ -283,12 +289,20 @@ def main():
         # correctness of the sharded path on this run: every rank's own z
         # entries must equal the unsharded apply's bitwise (no communication
         # needed: each rank checks its own slice, then one MIN over ranks)
+        # (the reference is an unsharded handle: this rank's own one factored
+        # only its shard's level-0 blocks and refuses the single-GPU apply)
+        P_full = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts, device=local)
         z_ref = torch.zeros_like(r)
-        P.PreconditioningDevice(z_ref, r, sptr)
+        P_full.PreconditioningDevice(z_ref, r, sptr)
         torch.cuda.synchronize()
         own = torch.from_numpy(P.maps()["s2o"][plan["vert_begin"]:plan["vert_end"]].astype(np.int64)).cuda()
         ok = torch.tensor([1.0 if torch.equal(z[own], z_ref[own]) else 0.0], device="cuda", dtype=torch.float64)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        del P_full
+        # Prepare: the slowest rank's steady-state phases
+        pt = torch.tensor([st0[k] for k in PREP_KEYS], device="cuda", dtype=torch.float64)
+        dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+        st0 = dict(st0, **dict(zip(PREP_KEYS, pt.tolist())))
         shard_check = {"own_slices_bitwise_equal_unsharded": bool(ok.item() == 1.0),
                        "form": "overlapped (fine during allgather)" if sharded.overlap else "serial"}
 
@@ -363,6 +377,8 @@ def main():
         "apply_algorithmic_GBps": round(apply_bytes / (t_max / args.steps) / 1e9, 1),
         "apply_bytes": apply_bytes,
         "prepare_ms": round(st0["prepare_ms"], 3),
+        "prepare_scope": (f"sharded Prepare, slowest of {world} ranks (own level-0 blocks + replicated coarse levels)"
+                          if sharded_path else "whole problem"),
         "prepare_first_call_ms": round(st_first["prepare_ms"], 3),
         "prepare_breakdown_ms": {"levels": round(st0["prepare_levels_ms"], 3),
                                  "assemble": round(st0["prepare_assemble_ms"], 3),

@@ -182,6 +182,14 @@ typedef struct {
 /* Host-only planner (no device needed): nbanks = ceil(nV/32); l1_first[b] =
  * first level-1 local id of level-0 bank b (b < nbanks), l1_first[nbanks] = n1. */
 int mas_shard_plan(int nV, const int* l1_first, int rank, int world, mas_shard* out);
+/* Sharded Prepare: every later Prepare of this handle assembles
+ * and factors only the level-0 blocks of shard `rank` of `world` (the same
+ * equal split of blocks as mas_shard_plan) and every coarse block; the level
+ * maps and the coarse assembly stay whole (they need every vertex).  Such a
+ * handle serves the sharded apply of that shard only; the single-GPU apply,
+ * the PCG driver and mas_save_blob then fail with MAS_ERR_STATE.  (0, 1)
+ * restores the whole Prepare. */
+int mas_set_prepare_shard(mas_handle h, int rank, int world);
 /* The same plan for a prepared handle. */
 int mas_shard_setup(mas_handle h, int rank, int world, mas_shard* out);
 int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r4, float* d_seg4, void* stream);

@@ -81,6 +81,8 @@ static std::vector<SecDesc> sections(mas_context* h) {
 
 int blob_size(mas_context* h, size_t* out) {
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "blob of an unprepared handle");
+    if (h->fineBlk0 != 0 || h->fineBlk1 != h->nFineBlk)
+        return fail(h, MAS_ERR_STATE, "blob of a shard-prepared handle (not every block is factored)");
     auto secs = sections(h);
     size_t n = align16(sizeof(MasBlobHeader)) + align16(secs.size() * sizeof(MasBlobSection));
     for (auto& d : secs) n += align16(d.bytes);
@@ -251,6 +253,7 @@ int blob_load(mas_context* h, const void* src, size_t size) {
     h->allocated = false;
     h->nV = hd.nV; h->nE = hd.nE; h->nF = hd.nF; h->L = hd.L; h->natL = hd.natL;
     h->totalClusters = hd.totalClusters; h->nBlk = hd.nBlk; h->nFineBlk = hd.nFineBlk;
+    h->fineBlk0 = 0; h->fineBlk1 = hd.nFineBlk;  // a blob holds every block's inverse
     h->maxNbr = hd.maxNbr; h->nStencil = hd.nStencil;
     std::memcpy(h->levelSize, hd.levelSize, sizeof(h->levelSize));
     const auto secs = sections(h);

@@ -2,7 +2,7 @@
 //
 //   k_aabb_partial / k_aabb_final  ComputeTotalAABB  (.cpp:193-211; SeAabbSimd.h:76-79)
 //   k_morton                       FillSortingData   (.cpp:219-235; SeMorton.h:75-101)
-//   hipcub radix sort (stable)     DoingSort         (.cpp:238-243; ties by index, B-9)
+//   onesweep radix sort (stable)   DoingSort         (.cpp:238-243; ties by index, B-9)
 //   k_inverse_map                  ComputeInverseMapper (.cpp:245-255)
 //   k_ell_map                      MapHessianTable   (.cpp:258-285)
 //
@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "mas_internal.h"
+#include "radix.h"
 
 namespace mas {
 
@@ -204,15 +205,8 @@ int run_allocate(mas_context* h, const float* pos4, const int* starts, const int
     k_aabb_final<<<1, kAabbBlock, 0, s>>>(P<float4>(h->aabbPartial), nPart);
     const float4* box = P<float4>(h->aabbPartial) + 2 * nPart;
     k_morton<<<cdiv(nV, 256), 256, 0, s>>>(P<float4>(h->pos), box, nV, P<uint64_t>(h->morton), P<int>(h->iota));
-    size_t tmp = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, P<uint64_t>(h->morton), P<uint64_t>(h->mortonSorted),
-                                       P<int>(h->iota), P<int>(h->s2o), nV, 0, 64, s);
-    if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
-    if ((rc = hip_check(h,
-                        hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, P<uint64_t>(h->morton),
-                                                           P<uint64_t>(h->mortonSorted), P<int>(h->iota),
-                                                           P<int>(h->s2o), nV, 0, 64, s),
-                        "radix sort")))
+    if ((rc = sort_pairs(h, P<uint64_t>(h->morton), P<uint64_t>(h->mortonSorted), P<int>(h->iota), P<int>(h->s2o), nV,
+                         64, s, "radix sort")))
         return rc;
     k_inverse_map<<<cdiv(nV, 256), 256, 0, s>>>(P<int>(h->s2o), nV, P<int>(h->o2s));
     if ((rc = hip_check(h, hipMemsetAsync(h->nbr.p, 0, (size_t)h->maxNbr * nV * 4, s), "memset nbr"))) return rc;

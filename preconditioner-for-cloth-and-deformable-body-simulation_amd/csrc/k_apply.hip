@@ -348,6 +348,9 @@ void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float
 
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     if (h->L >= 4 && !h->deepOff.p) return fail(h, MAS_ERR_STATE, "apply: deep-level lists not built");
+    if (h->fineBlk0 != 0 || h->fineBlk1 != h->nFineBlk)
+        return fail(h, MAS_ERR_STATE, "apply: the handle was prepared for one shard (mas_set_prepare_shard); "
+                                      "use the sharded apply of that shard");
     hipEvent_t* ev = nullptr;
     if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
     if (ev) hipEventRecord(ev[0], s);

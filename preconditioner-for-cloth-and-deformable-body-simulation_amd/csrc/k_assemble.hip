@@ -37,6 +37,7 @@
 #include <type_traits>
 
 #include "mas_internal.h"
+#include "radix.h"
 
 namespace mas {
 
@@ -264,15 +265,19 @@ __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* _
                                                      const float* __restrict__ off9, const int* __restrict__ ranges,
                                                      const float* __restrict__ additional,
                                                      float* __restrict__ dense, float* __restrict__ od,
-                                                     int* __restrict__ recCnt, FineContacts fc) {
+                                                     int* __restrict__ recCnt, FineContacts fc, int fb0, int fb1) {
     __shared__ __attribute__((aligned(16))) float tile[kDenseFloats];
     const int lane = threadIdx.x;
     const size_t blk = blockIdx.x;
+    // a sharded Prepare builds only its own blocks' tiles; od and the record
+    // counts (the coarse assembly's inputs) come from every block
+    const bool tiles = (int)blk >= fb0 && (int)blk < fb1;  // workgroup-uniform
     float4* gblk = reinterpret_cast<float4*>(dense + blk * kDenseFloats);
     float4* t4 = reinterpret_cast<float4*>(tile);
-    for (int q = lane; q < kDenseFloats / 4; q += 64) t4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tiles)
+        for (int q = lane; q < kDenseFloats / 4; q += 64) t4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
-    if (fc.off && lane < 9) {
+    if (tiles && fc.off && lane < 9) {
         const int r = lane / 3, c = lane % 3;
         const int j1 = fc.off[blk + 1];
         for (int j = fc.off[blk]; j < j1; ++j) {
@@ -293,8 +298,9 @@ __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* _
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);  // .cpp:1270
         float* e = tile + (3 * n) * 96 + 3 * n;  // .cpp:1271
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], acc[r * 3 + c]);
+        if (tiles)
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], acc[r * 3 + c]);
         const int num = nbrNum[v];
         const size_t base = (size_t)ranges[o];
         int cnt = 0;
@@ -316,8 +322,9 @@ __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* _
                 if (k0 + j >= num) break;
                 if ((ot[j] >> 5) == ((unsigned)v >> 5)) {  // same bank: level 0
                     float* t = tile + (3 * n) * 96 + 3 * (ot[j] & 31);
-                    for (int r = 0; r < 3; ++r)
-                        for (int c = 0; c < 3; ++c) t[r * 96 + c] = __fadd_rn(t[r * 96 + c], mm[j][c * 3 + r]);
+                    if (tiles)
+                        for (int r = 0; r < 3; ++r)
+                            for (int c = 0; c < 3; ++c) t[r * 96 + c] = __fadd_rn(t[r * 96 + c], mm[j][c * 3 + r]);
                     for (int r = 0; r < 3; ++r)
                         for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], mm[j][c * 3 + r]);
                 } else {
@@ -329,7 +336,8 @@ __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* _
         recCnt[v] = cnt;
     }
     __syncthreads();
-    for (int q = lane; q < kDenseFloats / 4; q += 64) gblk[q] = t4[q];
+    if (tiles)
+        for (int q = lane; q < kDenseFloats / 4; q += 64) gblk[q] = t4[q];
 }
 
 // Record keys pack (row, col) as coarse ids relative to level 1 in B bits each
@@ -747,18 +755,6 @@ static int exclusive_scan(mas_context* h, const T* in, T* out, int n, hipStream_
     return hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, in, out, n, s), what);
 }
 
-template <class K>
-static int sort_pairs(mas_context* h, const K* kin, K* kout, const int* vin, int* vout, int n, int bits,
-                      hipStream_t s, const char* what) {
-    if (n <= 0) return MAS_OK;
-    size_t tmp = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, n, 0, bits, s);
-    int rc = ensure(h, h->cubTemp, tmp);
-    if (rc) return rc;
-    return hip_check(h, hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, kin, kout, vin, vout, n, 0, bits, s),
-                     what);
-}
-
 int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
                    hipStream_t s, const char* what) {
     return sort_pairs(h, kin, kout, vin, vout, n, bits, s, what);
@@ -869,7 +865,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     FineContacts fc{};
     if (h->nStencil && (rc = run_contacts(h, s, fc))) return rc;
     k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
-                                              d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt), fc);
+                                              d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt), fc,
+                                              h->fineBlk0, h->fineBlk1);
     if (L == 1) return hip_check(h, hipGetLastError(), "assembly kernels");
 
     // coarse edge records in (u, k) order
@@ -912,17 +909,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         default: recordLaunch(std::integral_constant<int, 64>{}); break;
     }
     if (nRec > 0) {
-        tmp = 0;
-        hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, P<unsigned long long>(h->recKeys),
-                                           P<unsigned long long>(h->recKeysSorted), P<int>(h->recIds),
-                                           P<int>(h->recIdsSorted), nRec, 0, 2 * rk.B, s);
-        if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
-        if ((rc = hip_check(h,
-                            hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, P<unsigned long long>(h->recKeys),
-                                                               P<unsigned long long>(h->recKeysSorted),
-                                                               P<int>(h->recIds), P<int>(h->recIdsSorted), nRec, 0,
-                                                               2 * rk.B, s),
-                            "record sort")))
+        if ((rc = sort_pairs(h, P<unsigned long long>(h->recKeys), P<unsigned long long>(h->recKeysSorted),
+                             P<int>(h->recIds), P<int>(h->recIdsSorted), nRec, 2 * rk.B, s, "record sort")))
             return rc;
         k_fold_runs<DenseEntry, true, unsigned long long><<<cdiv(nRec, 64), 64, 0, s>>>(
             nRec, (1ull << (2 * rk.B)) - 1, P<unsigned long long>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
@@ -940,16 +928,10 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         const int beginPrev = h->levelSize[2 * (l - 1) + 1];
         const int* cstPrev = P<int>(h->cst) + (size_t)(l - 1) * nV;  // level-l local id per vertex
         const int* cstPrev2 = P<int>(h->cst) + (size_t)(l - 2) * nV; // level-(l-1) local id per vertex
-        tmp = 0;
         // keys are level-l local ids < count: sort only their bits
         const int vbits = std::max(1, bit_width((unsigned)std::max(count - 1, 0)));
-        hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, cstPrev, P<int>(h->vkeys), P<int>(h->iota), P<int>(h->vlist),
-                                           nV, 0, vbits, s);
-        if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
-        if ((rc = hip_check(h,
-                            hipcub::DeviceRadixSort::SortPairs(h->cubTemp.p, tmp, cstPrev, P<int>(h->vkeys),
-                                                               P<int>(h->iota), P<int>(h->vlist), nV, 0, vbits, s),
-                            "vertex-list sort")))
+        if ((rc = sort_pairs(h, reinterpret_cast<const unsigned*>(cstPrev), P<unsigned>(h->vkeys), P<int>(h->iota),
+                             P<int>(h->vlist), nV, vbits, s, "vertex-list sort")))
             return rc;
         k_bounds<<<cdiv(nV, 256), 256, 0, s>>>(nV, P<int>(h->vkeys), count, P<int>(h->voff));
         k_term_count<<<cdiv(nV + 1, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff), rec,

@@ -36,11 +36,11 @@ static_assert(kDenseFloats / 4 % kFactorThreads == 0, "factor load tiling");
 
 __global__ __launch_bounds__(kFactorThreads) void k_factor(const float* __restrict__ dense,
                                                           const unsigned* __restrict__ slotTable,
-                                                          float* __restrict__ inv) {
+                                                          float* __restrict__ inv, int blk0) {
     __shared__ __attribute__((aligned(16))) float A[96 * kLda];
     __shared__ float dinv[96];
     const int t = threadIdx.x;
-    const size_t blk = blockIdx.x;
+    const size_t blk = (size_t)blk0 + blockIdx.x;
     const float4* src = reinterpret_cast<const float4*>(dense + blk * kDenseFloats);
     for (int q = t; q < kDenseFloats / 4; q += kFactorThreads) {
         const int row = q / 24, c4 = q % 24;
@@ -206,9 +206,9 @@ struct ElimRB<96> {
 // the assembled blocks before the register-resident factor kernels (which
 // never see the whole block in one place).  mas_get_block_matrix reports the
 // same rule, so the stored blocks read back unchanged.
-__global__ __launch_bounds__(256) void k_identity_fix(float* __restrict__ dense, int nNodes) {
-    const int node = blockIdx.x * blockDim.x + threadIdx.x;
-    if (node >= nNodes) return;
+__global__ __launch_bounds__(256) void k_identity_fix(float* __restrict__ dense, int node0, int node1) {
+    const int node = node0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (node >= node1) return;
     float* d = dense + (size_t)(node >> 5) * kDenseFloats + (3 * (node & 31)) * 96 + 3 * (node & 31);
     if (*d != 0.0f) return;
     for (int i = 0; i < 3; ++i)
@@ -368,12 +368,12 @@ __device__ __forceinline__ void form_mfma(float* M, const float* dinv, float* ou
 template <bool MFMA>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_rb(
     const float* __restrict__ dense, float* __restrict__ inv, const uint4* __restrict__ tileSlot,
-    const uint4* __restrict__ valuSlot) {
+    const uint4* __restrict__ valuSlot, int blk0) {
     __shared__ __attribute__((aligned(16))) float M[kPackedM];
     __shared__ __attribute__((aligned(16))) float piv[96];
     __shared__ float dinv[96];
     const int t = threadIdx.x;
-    const size_t blk = blockIdx.x;
+    const size_t blk = (size_t)blk0 + blockIdx.x;
     const int rg = t >> 2, cg = t & 3;
     float v[6][24];
     {
@@ -475,14 +475,20 @@ int run_factor(mas_context* h, hipStream_t s) {
     if (rc) return rc;
     float* dense = P<float>(h->dense);
     float* inv = P<float>(h->inv);
-    if (h->factorVariant == 0) {
-        k_factor<<<h->nBlk, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv);
-    } else {
-        k_identity_fix<<<cdiv(h->nBlk * 32, 256), 256, 0, s>>>(dense, h->nBlk * 32);
-        if (h->factorVariant == 3)
-            k_factor_rb<true><<<h->nBlk, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot));
-        else
-            k_factor_rb<false><<<h->nBlk, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot));
+    // the prepared level-0 blocks (all, or a shard's), then every coarse block
+    const int ranges[2][2] = {{h->fineBlk0, h->fineBlk1}, {h->nFineBlk, h->nBlk}};
+    for (const auto& rg : ranges) {
+        const int b0 = rg[0], nb = rg[1] - rg[0];
+        if (nb <= 0) continue;
+        if (h->factorVariant == 0) {
+            k_factor<<<nb, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv, b0);
+        } else {
+            k_identity_fix<<<cdiv(nb * 32, 256), 256, 0, s>>>(dense, b0 * 32, rg[1] * 32);
+            if (h->factorVariant == 3)
+                k_factor_rb<true><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0);
+            else
+                k_factor_rb<false><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0);
+        }
     }
     return hip_check(h, hipGetLastError(), "factor kernel");
 }

@@ -256,6 +256,14 @@ static int shard_coarse(mas_context* h, const mas_shard& sh, int world, const fl
     return MAS_OK;
 }
 
+// the shard's level-0 blocks must be among those the last Prepare factored
+static int check_fine_prepared(mas_context* h, const mas_shard& sh) {
+    if (sh.fine_block_begin < h->fineBlk0 || sh.fine_block_end > h->fineBlk1)
+        return fail(h, MAS_ERR_STATE, "sharded apply: level-0 blocks [" + std::to_string(sh.fine_block_begin) + ", " +
+                                          std::to_string(sh.fine_block_end) + ") were not prepared on this handle");
+    return MAS_OK;
+}
+
 static hipEvent_t* shard_events(mas_context* h) {
     return h->profiling && h->profRecorded < kProfRing ? &h->prof[4 * h->profRecorded++] : nullptr;
 }
@@ -267,6 +275,7 @@ int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gat
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
     if (rc) return rc;
+    if ((rc = check_fine_prepared(h, sh))) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     const float4* r = reinterpret_cast<const float4*>(d_r4);
     float4* z = reinterpret_cast<float4*>(d_z4);
@@ -290,6 +299,7 @@ int mas_apply_shard_fine(mas_handle h, int rank, int world, const float* d_r4, f
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
     if (rc) return rc;
+    if ((rc = check_fine_prepared(h, sh))) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     hipEvent_t* ev = shard_events(h);
     h->shardPendingEv = ev;

@@ -348,6 +348,8 @@ int mas_get_block_matrix(mas_handle h, int blk, float* out96) {
     if (!h->prepared || h->fromBlob || !h->dense.p)
         return fail(h, MAS_ERR_STATE, "block matrix before prepare (a restored blob holds no assembly blocks)");
     if (blk < 0 || blk >= h->nBlk) return fail(h, MAS_ERR_ARG, "block index out of range");
+    if (blk < h->nFineBlk && (blk < h->fineBlk0 || blk >= h->fineBlk1))
+        return fail(h, MAS_ERR_STATE, "level-0 block outside the shard this handle was prepared for");
     hipSetDevice(h->device);
     hipStreamSynchronize(h->stream);
     MAS_TRY(hip_check(h, hipMemcpy(out96, P<float>(h->dense) + (size_t)blk * kDenseFloats, kDenseFloats * 4,
@@ -365,6 +367,8 @@ int mas_get_block_inverse(mas_handle h, int blk, float* out96) {
     if (!h || !out96) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "block inverse before prepare");
     if (blk < 0 || blk >= h->nBlk) return fail(h, MAS_ERR_ARG, "block index out of range");
+    if (blk < h->nFineBlk && (blk < h->fineBlk0 || blk >= h->fineBlk1))
+        return fail(h, MAS_ERR_STATE, "level-0 block outside the shard this handle was prepared for");
     hipSetDevice(h->device);
     hipStreamSynchronize(h->stream);
     return copy_block_inverse(h, blk, out96);
@@ -378,6 +382,14 @@ int mas_get_coarse_residual(mas_handle h, float* out4) {
     hipSetDevice(h->device);
     hipDeviceSynchronize();  // the apply may have run on any stream
     return hip_check(h, hipMemcpy(out4, h->Rc.p, (size_t)nCoarse * 16, hipMemcpyDeviceToHost), "D2H Rc");
+}
+
+int mas_set_prepare_shard(mas_handle h, int rank, int world) {
+    if (!h) return MAS_ERR_ARG;
+    if (world < 1 || rank < 0 || rank >= world) return fail(h, MAS_ERR_ARG, "mas_set_prepare_shard: bad rank/world");
+    h->prepRank = rank;
+    h->prepWorld = world;
+    return MAS_OK;
 }
 
 }  // extern "C"

@@ -94,6 +94,10 @@ struct mas_context {
     int coarseMode = 2;
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
+    // sharded Prepare (mas_set_prepare_shard): the next Prepare assembles and
+    // factors only the level-0 blocks of Morton shard prepRank / prepWorld;
+    // [fineBlk0, fineBlk1) = the level-0 blocks the last Prepare factored
+    int prepRank = 0, prepWorld = 1, fineBlk0 = 0, fineBlk1 = 0;
     int levelSize[2 * 9] = {};
 
     // allocate-phase device data

@@ -23,6 +23,10 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     if (!ev.ok()) return fail(h, MAS_ERR_HIP, "hipEventCreate");
     hipEvent_t e0 = ev.e[0], e1 = ev.e[1];
     if ((rc = run_levels(h, s))) return rc;
+    // the level-0 blocks this Prepare assembles and factors: all, or those of
+    // the Morton shard set by mas_set_prepare_shard (mas_shard_plan's split)
+    h->fineBlk0 = (int)((long long)h->prepRank * h->nFineBlk / h->prepWorld);
+    h->fineBlk1 = (int)((long long)(h->prepRank + 1) * h->nFineBlk / h->prepWorld);
     hipEventRecord(e0, s);
     if ((rc = run_assemble(h, d_diag9, d_off9, d_ranges, s))) return rc;
     hipEventRecord(e1, s);

@@ -36,7 +36,7 @@ ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_allocate", "mas_prepare",
            "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_get_info",
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
-           "mas_get_coarse_residual",
+           "mas_get_coarse_residual", "mas_set_prepare_shard",
            "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
            "mas_apply_shard_fine", "mas_apply_shard_complete", "mas_shard_apply_device", "mas_rccl_unique_id",
            "mas_rccl_init", "mas_shard_apply_rccl",
@@ -122,6 +122,7 @@ def lib():
         L.mas_get_block_matrix.argtypes = [P, I, P]
         L.mas_get_block_inverse.argtypes = [P, I, P]
         L.mas_get_coarse_residual.argtypes = [P, P]
+        L.mas_set_prepare_shard.argtypes = [P, I, I]
         L.mas_shard_plan.argtypes = [I, P, I, I, ctypes.POINTER(mas_shard)]
         L.mas_shard_setup.argtypes = [P, I, I, ctypes.POINTER(mas_shard)]
         L.mas_apply_shard_restrict.argtypes = [P, I, I, P, P, P]
@@ -466,6 +467,10 @@ class SeSchwarzPreconditioner:
         self._check(self._L.mas_get_block_inverse(self.h, blk, _ptr(B)), "get_block_inverse")
         return B
 
+    def set_prepare_shard(self, rank: int, world: int):
+        """Later Prepares factor only the level-0 blocks of shard rank/world (mas_set_prepare_shard)."""
+        self._check(self._L.mas_set_prepare_shard(self.h, int(rank), int(world)), "set_prepare_shard")
+
     def coarse_residual(self):
         """R of every coarse node (ids begin_1 .. total_clusters-1) after the last apply, [n, 4] float32."""
         info = self.info()
@@ -477,9 +482,12 @@ class SeSchwarzPreconditioner:
         return R
 
 
-def from_mesh(mesh, max_levels=0, contacts=None, **kw) -> SeSchwarzPreconditioner:
-    """Allocate + Prepare a preconditioner for a meshgen.Mesh (host path)."""
+def from_mesh(mesh, max_levels=0, contacts=None, shard=None, **kw) -> SeSchwarzPreconditioner:
+    """Allocate + Prepare a preconditioner for a meshgen.Mesh (host path).
+    shard=(rank, world): a sharded Prepare (only that shard's level-0 blocks)."""
     P = SeSchwarzPreconditioner(max_levels=max_levels, **kw)
+    if shard is not None:
+        P.set_prepare_shard(*shard)
     P.m_positions = mesh.pos
     P.m_neighbours = (mesh.starts, mesh.idx)
     P.m_edges = mesh.edges

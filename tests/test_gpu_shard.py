@@ -36,6 +36,16 @@ def _virtual_sharded(P, r, world, overlap=False):
     return z
 
 
+def _unsharded(P, r):
+    import torch
+    z = torch.zeros_like(r)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    P.PreconditioningDevice(z, r, s.cuda_stream)
+    s.synchronize()
+    return z
+
+
 @pytest.mark.parametrize("kind,W,L,worlds,nc", [("cloth", 64, 0, (1, 2, 3, 8), 0), ("cloth", 100, 1, (2, 5), 0),
                                                 ("tet", 16, 3, (2, 4), 0), ("cloth", 1024, 4, (2, 8), 0),
                                                 ("cloth", 1024, 4, (8,), 100_000), ("tet", 160, 4, (8,), 0)])
@@ -58,6 +68,53 @@ def test_virtual_shards_bitwise(kind, W, L, worlds, nc):
         for overlap in (False, True):
             z = _virtual_sharded(P, r, world, overlap)
             assert torch.equal(z, z_ref), (world, overlap, float((z - z_ref).abs().max()))
+
+
+@pytest.mark.parametrize("kind,W,L,world,nc", [("cloth", 100, 3, 3, 0), ("tet", 16, 3, 2, 0),
+                                               ("cloth", 1024, 4, 8, 100_000), ("tet", 160, 4, 8, 0)])
+def test_shard_prepared_handles_bitwise(kind, W, L, world, nc):
+    """Sharded Prepare (mas_set_prepare_shard): rank g's handle
+    assembles and factors only its own level-0 blocks (plus the replicated
+    coarse levels); its restrict and finish reproduce the unsharded apply's z
+    on its vertices bit for bit, and its factor phase shrinks with the world.
+    Such a handle refuses the single-GPU apply, other shards and other ranks'
+    level-0 blocks.  Includes BASELINE configs[3] (1M + 100k VF contacts) and
+    configs[4] (4M tet lattice) at 8 ranks."""
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(W) if kind == "cloth" else tet(W)
+    contacts = meshgen.vf_contacts(mesh, nc, seed=3) if nc else None
+    Pf = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 6)).cuda()
+    z_ref = _unsharded(Pf, r)
+    t_full = Pf.stats()["prepare_factor_ms"]
+    ranks = [mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, shard=(g, world)) for g in range(world)]
+    s = torch.cuda.Stream()
+    plans = [Pg.shard_setup(g, world) for g, Pg in enumerate(ranks)]
+    seg = plans[0]["seg_max"]
+    with torch.cuda.stream(s):
+        segs = [torch.zeros((seg, 4), dtype=torch.float32, device="cuda") for _ in range(world)]
+        for g, Pg in enumerate(ranks):
+            Pg.shard_restrict(g, world, r, segs[g], s.cuda_stream)
+        gathered = torch.cat(segs, 0).contiguous()
+        z = torch.full_like(r, float("nan"))
+        for g, Pg in enumerate(ranks):
+            Pg.shard_finish(g, world, gathered, r, z, s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(z, z_ref), float((z - z_ref).abs().max())
+    t_rank = max(Pg.stats()["prepare_factor_ms"] for Pg in ranks)
+    print(f"factor phase: unsharded {t_full:.3f} ms, slowest of {world} ranks {t_rank:.3f} ms")
+    if mesh.nV >= 1_000_000:
+        assert t_rank < 0.35 * t_full, (t_rank, t_full)
+    P1 = ranks[1]
+    with pytest.raises(mas_amd.MasError, match="STATE"):
+        P1.PreconditioningDevice(torch.zeros_like(r), r, s.cuda_stream)
+    with pytest.raises(mas_amd.MasError, match="STATE"):
+        P1.shard_finish(0, world, gathered, r, z, s.cuda_stream)
+    with pytest.raises(mas_amd.MasError, match="STATE"):
+        P1.block_inverse(0)
+    P1.block_inverse(plans[1]["fine_block_begin"])
 
 
 def test_sharded_apply_helper_world1():
