@@ -130,7 +130,7 @@ def cpu_baseline(mesh, cfg, contacts, r_np, steps):
                       f"ms/apply {med * 1e3:.2f}"}, z
 
 
-PREP_KEYS = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms")
+PREP_KEYS = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms", "prepare_fine_ms")
 
 
 def main():
@@ -382,7 +382,8 @@ def main():
         "prepare_first_call_ms": round(st_first["prepare_ms"], 3),
         "prepare_breakdown_ms": {"levels": round(st0["prepare_levels_ms"], 3),
                                  "assemble": round(st0["prepare_assemble_ms"], 3),
-                                 "factor": round(st0["prepare_factor_ms"], 3)},
+                                 "factor": round(st0["prepare_factor_ms"], 3),
+                                 "level0_fused_overlapped": round(st0["prepare_fine_ms"], 3)},
         "allocate_ms": round(st0["allocate_ms"], 3),
         "host_setup_s": round(setup_s, 2),
         "wall_s_timed": round(wall, 4),

@@ -61,7 +61,10 @@ typedef struct {
     int resort_period; /* 0 = reference behaviour (sort on first Allocate only, B-1); k>0: re-sort every k calls */
     int fix_vf_bary;   /* 0 = parity with reference release build (B-2); 1 = -(1-b0-b1) */
     int device;        /* HIP device ordinal; -1 = current device */
-    int reserved[12];
+    int keep_blocks;   /* 1 = Prepare also stores the assembled level-0 blocks (mas_get_block_matrix on
+                          them; +2.4 GB of HBM traffic at 1M).  0 = the fused level-0 assemble + factor
+                          never writes them; only the coarse blocks are kept */
+    int reserved[11];
 } mas_config;
 
 typedef struct {
@@ -92,6 +95,12 @@ typedef struct {
     double post_fine_ms_avg;   /* after it (0 on the single-GPU path: the prolongation is fused) */
     int64_t apply_mode;        /* coarse levels: 2 = restrictions then all solves, two launches
                                   (default); 0 = one launch per level */
+    /* Prepare phases: levels = stencils + aggregation; assemble = contacts + the coarse
+       assembly (+ the level-0 assembly when unfused); factor = the rest (coarse factor,
+       apply tables; + the level-0 factor when unfused).  The fused level-0 assemble +
+       factor (default) runs on its own stream beside assemble/factor: prepare_fine_ms
+       is its device time (0 when unfused) */
+    double prepare_fine_ms;
 } mas_stats;
 
 /* lifecycle */

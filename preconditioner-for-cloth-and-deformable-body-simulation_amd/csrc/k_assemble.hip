@@ -34,6 +34,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
+#include <vector>
 #include <type_traits>
 
 #include "mas_internal.h"
@@ -340,6 +342,48 @@ __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* _
         for (int q = lane; q < kDenseFloats / 4; q += 64) gblk[q] = t4[q];
 }
 
+// od(v) and the coarse record count of every vertex, one thread per vertex:
+// k_level0_block's per-vertex sums without the tile (the fused variant builds
+// the tiles inside k_factor_fused).  od = diag + additional, then the
+// same-bank neighbour blocks in ELL order (.cpp:1270-1282).
+__global__ __launch_bounds__(256) void k_od(FineAsm a, float* __restrict__ od, int* __restrict__ recCnt) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= a.nV) return;
+    const int o = a.s2o[v];
+    float acc[9];
+    const float* d = a.diag9 + 9 * (size_t)o;
+    const float* ad = a.additional + 9 * (size_t)v;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);
+    const int num = a.nbrNum[v];
+    const size_t base = (size_t)a.ranges[o];
+    int cnt = 0;
+    for (int k0 = 1; k0 < num; k0 += 4) {  // every load of a chunk first; cross-bank blocks are not read
+        bool same[4];
+        float mm[4][9];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = k0 + j;
+            const unsigned ot = k < num ? (unsigned)a.nbr[(size_t)k * a.nV + v] : 0xffffffffu;
+            same[j] = k < num && (ot >> 5) == ((unsigned)v >> 5);
+            cnt += k < num && !same[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float* m = a.off9 + 9 * (base + k0 + j - 1);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) mm[j][q] = same[j] ? m[q] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (same[j])
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) acc[r * 3 + c] = __fadd_rn(acc[r * 3 + c], mm[j][c * 3 + r]);
+    }
+    for (int q = 0; q < 9; ++q) od[9 * (size_t)v + q] = acc[q];
+    recCnt[v] = cnt;
+}
+
 // Record keys pack (row, col) as coarse ids relative to level 1 in B bits each
 // (B = bit width of the coarse node count, 16 at 1M): the stable radix sort
 // then runs over 2B bits instead of 64 (4 passes instead of 8 at 1M).  A dead
@@ -444,17 +488,22 @@ struct DenseEntry {  // block entry (row node, column node) of the dense buffer
     float* dense;
     RecKey rk;
     static constexpr int kStride = 96;
-    __device__ float* at(unsigned long long k) const { return entry(dense, rk.row(k), rk.col(k)); }
+    __device__ float* at(unsigned long long k, int) const { return entry(dense, rk.row(k), rk.col(k)); }
 };
 struct DenseDiag {  // the diagonal entry of a node
     float* dense;
     static constexpr int kStride = 96;
-    __device__ float* at(unsigned k) const { return entry(dense, k, k); }
+    __device__ float* at(unsigned k, int) const { return entry(dense, k, k); }
 };
 struct NodeRow {  // a row-major 9-float row per node (additional)
     float* base;
     static constexpr int kStride = 3;
-    __device__ float* at(unsigned k) const { return base + 9 * (size_t)k; }
+    __device__ float* at(unsigned k, int) const { return base + 9 * (size_t)k; }
+};
+struct RunSlot {  // a row-major 3x3 per run, at the run's first sorted position (FineAsm::cval)
+    float* base;
+    static constexpr int kStride = 3;
+    __device__ float* at(unsigned long long, int start) const { return base + 9 * (size_t)start; }
 };
 
 // One wave per 64 sorted positions: the lanes find the runs starting there;
@@ -482,7 +531,7 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __
         isLong = isStart && i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key;
     }
     if (isStart && !isLong) {  // short run: this lane, loads batched kFoldBatch at a time
-        float* e = tgt.at(key);
+        float* e = tgt.at(key, i);
         float acc[9];
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * S + c];
@@ -512,7 +561,7 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __
     for (unsigned long long starts = __ballot(isLong); starts; starts &= starts - 1) {
         const int start = blockIdx.x * 64 + __ffsll((long long)starts) - 1;
         const Key lkey = keys[start];
-        float* e = tgt.at(lkey);
+        float* e = tgt.at(lkey, start);
         float acc = lane < 9 ? e[r * S + c] : 0.f;
         for (int j0 = start;; j0 += 64) {
             const int j = j0 + lane;
@@ -760,11 +809,50 @@ int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const in
     return sort_pairs(h, kin, kout, vin, vout, n, bits, s, what);
 }
 
+// Fused variant: k_factor_fused over the prepared level-0 blocks on
+// prepStream, after everything this stream has queued (its inputs: additional
+// and the prefolded level-0 contact entries); run_factor joins.  With
+// MAS_PREP_CU_RESERVE=k the side stream leaves k CUs to the coarse assembly
+// (a CU-masked queue), which otherwise waits for the fused kernel's slots.
+static int fork_fused(mas_context* h, const FineAsm& fa, hipStream_t s) {
+    int rc;
+    if (!h->prepStream) {
+        int reserve = 0;
+        if (const char* e = std::getenv("MAS_PREP_CU_RESERVE")) reserve = std::atoi(e);
+        hipDeviceProp_t prop{};
+        if (reserve > 0 && hipGetDeviceProperties(&prop, h->device) == hipSuccess &&
+            reserve < prop.multiProcessorCount) {
+            const int n = prop.multiProcessorCount, words = (n + 31) / 32;
+            std::vector<uint32_t> mask(words, 0);
+            for (int cu = 0; cu < n - reserve; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+            rc = hip_check(h, hipExtStreamCreateWithCUMask(&h->prepStream, words, mask.data()), "prepare stream");
+        } else {
+            rc = hip_check(h, hipStreamCreateWithFlags(&h->prepStream, hipStreamNonBlocking), "prepare stream");
+        }
+        if (rc || (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepFork, hipEventDisableTiming), "event")) ||
+            (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepJoin, hipEventDisableTiming), "event")) ||
+            (rc = hip_check(h, hipEventCreate(&h->evFine[0]), "event")) ||
+            (rc = hip_check(h, hipEventCreate(&h->evFine[1]), "event")))
+            return rc;
+    }
+    // MAS_PREP_SERIAL=1 (A/B): the same kernel in line on the caller's stream
+    static const bool serial = std::getenv("MAS_PREP_SERIAL") && std::atoi(std::getenv("MAS_PREP_SERIAL"));
+    hipStream_t ps = serial ? s : h->prepStream;
+    if ((rc = hip_check(h, hipEventRecord(h->evPrepFork, s), "fork")) ||
+        (rc = hip_check(h, hipStreamWaitEvent(ps, h->evPrepFork, 0), "fork wait")) ||
+        (rc = hip_check(h, hipEventRecord(h->evFine[0], ps), "record")) ||
+        (rc = launch_factor_fused(h, fa, h->fineBlk0, h->fineBlk1, ps)) ||
+        (rc = hip_check(h, hipEventRecord(h->evFine[1], ps), "record")) ||
+        (rc = hip_check(h, hipEventRecord(h->evPrepJoin, ps), "join")))
+        return rc;
+    return MAS_OK;
+}
+
 // The contact part of the assembly in the reference's single-thread order
 // (see "contacts" above): on return the coarse blocks hold the contact block
 // entries and the additional pushes, `additional` holds every node's contact
 // row, and fc points k_level0_block at the fine block entries.
-static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc) {
+static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm& fa, bool& forked) {
     const int n = h->nStencil, L = h->L, tc = h->totalClusters, begin1 = L > 1 ? h->levelSize[3] : tc;
     const int B = std::max(1, bit_width((unsigned)(tc - 1)));
     const int* gn = P<int>(h->goingNext);
@@ -801,7 +889,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc) {
         (rc = sort_pairs(h, P<unsigned>(h->caKeys), P<unsigned>(h->caKeysS), P<int>(h->caIds), P<int>(h->caIdsS), nA,
                          B, s, "contact row sort")))
         return rc;
-    float* dense = P<float>(h->dense);
+    float* dense = dense_base(h);
     // fine entries: k_level0_block; coarse entries: folded onto the zeroed coarse blocks
     k_contact_fine_bounds<<<cdiv(nD + 1, 256), 256, 0, s>>>(nD, B, begin1, h->nFineBlk,
                                                             P<unsigned long long>(h->cdKeysS), P<int>(h->cFineOff));
@@ -820,6 +908,27 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc) {
     if ((rc = hip_check(h, hipMemcpyAsync(&nP, P<int>(h->cpOff) + nA, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
         (rc = hip_check(h, hipStreamSynchronize(s), "push count sync")))
         return rc;
+    fc = FineContacts{P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
+                      B};
+    if (h->factorVariant == 4) {
+        if (fineEnd > 0) {
+            // each level-0 entry's contact run folded from zero once, stored at
+            // the run's first position (the fused kernel adds it to its zero entry)
+            if ((rc = ensure(h, h->cFineVal, (size_t)fineEnd * 36)) ||
+                (rc = hip_check(h, hipMemsetAsync(h->cFineVal.p, 0, (size_t)fineEnd * 36, s), "memset fine contacts")))
+                return rc;
+            k_fold_runs<RunSlot, true, unsigned long long><<<cdiv(fineEnd, 64), 64, 0, s>>>(
+                fineEnd, ~0ull, P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal),
+                RunSlot{P<float>(h->cFineVal)});
+            fa.ckeys = P<unsigned long long>(h->cdKeysS);
+            fa.cval = P<float>(h->cFineVal);
+            fa.coff = P<int>(h->cFineOff);
+            fa.B = B;
+        }
+        // the level-0 blocks need nothing below: they start now
+        if ((rc = fork_fused(h, fa, s))) return rc;
+        forked = true;
+    }
     const RecKey rk{0, B};
     if (nD > fineEnd)
         k_fold_runs<DenseEntry, true, unsigned long long><<<cdiv(nD - fineEnd, 64), 64, 0, s>>>(
@@ -838,35 +947,49 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc) {
         k_fold_runs<DenseDiag, false, unsigned><<<cdiv(nP, 64), 64, 0, s>>>(
             nP, 0xffffffffu, P<unsigned>(h->cpKeysS), P<int>(h->cpIdsS), P<float>(h->additional), DenseDiag{dense});
     }
-    fc = FineContacts{P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
-                      B};
     return hip_check(h, hipGetLastError(), "contact kernels");
 }
 
 int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s) {
     const int nV = h->nV, L = h->L, tc = h->totalClusters;
     int rc;
-    const size_t denseBytes = (size_t)h->nBlk * kDenseFloats * 4;
-    if ((rc = ensure(h, h->dense, denseBytes)) || (rc = ensure(h, h->additional, (size_t)(tc + 1) * 36)) ||
+    const bool fused = h->factorVariant == 4;
+    // the fused factor never stores level-0 blocks unless asked to keep them
+    h->denseFine = !fused || h->cfg.keep_blocks;
+    const int nStored = h->denseFine ? h->nBlk : h->nBlk - h->nFineBlk;
+    const size_t denseBytes = (size_t)std::max(nStored, 1) * kDenseFloats * 4;
+    if ((rc = ensure(h, h->dense, denseBytes)) || (rc = ensure(h, h->inv, (size_t)h->nBlk * kBlockFloats * 4)) ||
+        (rc = ensure(h, h->additional, (size_t)(tc + 1) * 36)) ||
         (rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
         (rc = ensure(h, h->recOff, (size_t)(nV + 1) * 4)) || (rc = ensure(h, h->tab, (size_t)(tc + 1) * 36)))
         return rc;
-    // fine blocks are written whole by k_level0_block: zero only the coarse blocks
-    const size_t zeroFrom = (size_t)h->nFineBlk * kDenseFloats * 4;
-    if ((denseBytes > zeroFrom &&
-         (rc = hip_check(h, hipMemsetAsync(static_cast<char*>(h->dense.p) + zeroFrom, 0, denseBytes - zeroFrom, s),
+    // level-0 blocks are written whole (or never stored): zero only the coarse blocks
+    const size_t zeroFrom = h->denseFine ? (size_t)h->nFineBlk * kDenseFloats * 4 : 0;
+    const size_t coarseBytes = (size_t)(h->nBlk - h->nFineBlk) * kDenseFloats * 4;
+    if ((coarseBytes > 0 &&
+         (rc = hip_check(h, hipMemsetAsync(static_cast<char*>(h->dense.p) + zeroFrom, 0, coarseBytes, s),
                          "memset dense"))) ||
         (rc = hip_check(h, hipMemsetAsync(h->additional.p, 0, (size_t)(tc + 1) * 36, s), "memset additional")) ||
         (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt")))
         return rc;
-    float* dense = P<float>(h->dense);
+    float* dense = dense_base(h);
     float* add = P<float>(h->additional);
     const int* gn = P<int>(h->goingNext);
     FineContacts fc{};
-    if (h->nStencil && (rc = run_contacts(h, s, fc))) return rc;
-    k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
-                                              d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt), fc,
-                                              h->fineBlk0, h->fineBlk1);
+    FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges, add,
+               nullptr, nullptr, nullptr, 0, h->cfg.keep_blocks ? dense : nullptr};
+    bool forked = false;
+    if (h->nStencil && (rc = run_contacts(h, s, fc, fa, forked))) return rc;
+    if (fused) {
+        // the level-0 blocks assemble and factor on prepStream while this
+        // stream assembles the coarse levels (run_factor joins)
+        if (!forked && (rc = fork_fused(h, fa, s))) return rc;
+        k_od<<<cdiv(nV, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+    } else {
+        k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
+                                                  d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt),
+                                                  fc, h->fineBlk0, h->fineBlk1);
+    }
     if (L == 1) return hip_check(h, hipGetLastError(), "assembly kernels");
 
     // coarse edge records in (u, k) order

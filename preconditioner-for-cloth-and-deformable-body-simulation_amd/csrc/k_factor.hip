@@ -114,13 +114,19 @@ __device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float* di
         for (int c4 = 0; c4 < 6; ++c4)
             *reinterpret_cast<float4*>(&pr[24 * cg + 4 * c4]) =
                 make_float4(v[mX][4 * c4], v[mX][4 * c4 + 1], v[mX][4 * c4 + 2], v[mX][4 * c4 + 3]);
-        if (cg == cgX) dinv[X] = __fdiv_rn(1.0f, v[mX][cX]);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // the pivot is final from this step on: D^-1_X (.cpp:1429-1433) here, by
+    // every lane (no divergent branch; measured 1.75 vs 1.86 ms at 1M with the
+    // division in the pivot lane's branch)
+    const float pd = pr[X];
+    {
+        const float d = __fdiv_rn(1.0f, pd);
+        if (rg == 0 && cg == 0) dinv[X] = d;
+    }
     if constexpr (mLo <= 5) {
-        const float pd = pr[X];
         float a[6], r[6];
 #pragma unroll
         for (int m = mLo; m < 6; ++m) a[m] = quad_bcast(v[m][cX], cgX);
@@ -136,6 +142,8 @@ __device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float* di
             }
             const bool act0 = m0 < 6 && rg + 16 * m0 > X && a0 != 0.0f;
             const bool act1 = m1 < 6 && rg + 16 * m1 > X && a1 != 0.0f;
+            // (a shared-reciprocal division without the scale / fixup steps,
+            // exact for operands in [2^-40, 2^40], measured 11 % slower)
             if (act0) q0 = __fdiv_rn(-a0, pd);
             if (act1) q1 = __fdiv_rn(-a1, pd);
         }
@@ -361,6 +369,39 @@ __device__ __forceinline__ void form_mfma(float* M, const float* dinv, float* ou
     for (int q = lane; q < kBlockF4; q += 64) out4[q] = O4[q];
 }
 
+// The block in the lane tiles v (lane t: rows t / 4 + 16 m, columns
+// 24 (t % 4) .. + 23) -> elimination, M, the packed inverse at out.
+template <bool MFMA>
+__device__ __forceinline__ void factor_tiles(float (&v)[6][24], float* M, float* piv, float* dinv, float* out,
+                                             const uint4* __restrict__ tileSlot, const uint4* __restrict__ valuSlot,
+                                             int t) {
+    const int rg = t >> 2, cg = t & 3;
+    ElimRB<0>::run(v, piv, dinv, rg, cg);
+    // M rows: unit diagonal, L^-1 below, only the stored (padded) columns
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const int k = rg + 16 * m, len = (k & ~3) + 4;
+#pragma unroll
+        for (int c4 = 0; c4 < 6; ++c4) {
+            const int col = 24 * cg + 4 * c4;
+            if (col < len) {
+                float4 q = make_float4(v[m][4 * c4], v[m][4 * c4 + 1], v[m][4 * c4 + 2], v[m][4 * c4 + 3]);
+                if (col == (k & ~3)) {  // the diagonal lies in this float4
+                    const int d = k & 3;
+                    q.x = d == 0 ? 1.f : q.x;
+                    q.y = d == 1 ? 1.f : q.y;
+                    q.z = d == 2 ? 1.f : q.z;
+                    q.w = d == 3 ? 1.f : q.w;
+                }
+                *reinterpret_cast<float4*>(&M[m_row(k) + col]) = q;
+            }
+        }
+    }
+    __syncthreads();
+    if (MFMA) form_mfma(M, dinv, out, tileSlot, t);  // one wave: no barrier around M
+    else form_packed_staged(M, dinv, out, valuSlot, t);
+}
+
 // Register-blocked factor: LDS holds only the pivot row, D^-1 and the packed
 // M (~19.5 KB -> 8 blocks per CU at <= 256 VGPRs), the block is loaded from
 // HBM straight into the lane tiles, and M's LDS is reused to stage the packed
@@ -390,30 +431,151 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 v[m][4 * c4 + 3] = q.w;
             }
     }
-    ElimRB<0>::run(v, piv, dinv, rg, cg);
-    // M rows: unit diagonal, L^-1 below, only the stored (padded) columns
+    factor_tiles<MFMA>(v, M, piv, dinv, inv + blk * kBlockFloats, tileSlot, valuSlot, t);
+}
+
+// ---------------------------------------------------------------------------
+// Fused level-0 assemble + factor (the default, MAS_FACTOR_VARIANT=4)
+// ---------------------------------------------------------------------------
+//
+// One wave per level-0 block builds the block in two LDS slabs of 16 nodes
+// (48 rows x 96 columns, 18 KB, aliased with the factor's packed M, so LDS
+// stays ~20 KB and two waves per SIMD still fit), moves each slab into the
+// factor's lane tiles and factors as k_factor_rb.  The assembled block never
+// reaches HBM: 2 x 36 KB of traffic per block less than k_level0_block +
+// k_factor_rb (2.4 GB at 1M), and the assembly's load latency hides behind the
+// other wave's elimination.  Per entry the sums are the reference's: the
+// block's contact entries first (one prefolded run sum per entry, added to
+// zero), then the CSR terms in ELL order -- the diagonal node's
+// diag + additional (.cpp:1270-1271), each same-bank neighbour's off-diagonal
+// (.cpp:1275-1282) -- then the zero-diagonal identity rule (.cpp:1365-1368).
+// Bitwise equal to k_level0_block + k_identity_fix + k_factor_rb.
+template <int H>
+__device__ __forceinline__ void build_slab(const FineAsm& a, int blk, float* S, int lane) {
+    float4* S4 = reinterpret_cast<float4*>(S);
+    for (int q = lane; q < 48 * 96 / 4; q += 64) S4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    if (a.ckeys) {  // contact entries of rows in this slab: distinct keys -> distinct entries
+        const int j1 = a.coff[blk + 1];
+        const unsigned long long colMask = (1ull << a.B) - 1;
+        for (int j = a.coff[blk] + lane; j < j1; j += 64) {
+            const unsigned long long key = a.ckeys[j];
+            const bool start = j == 0 || a.ckeys[j - 1] != key;
+            const int nl = (int)((key >> a.B) & 31) - 16 * H, col = (int)(key & colMask) & 31;
+            if (start && nl >= 0 && nl < 16) {
+                const float* src = a.cval + 9 * (size_t)j;
+                float* e = S + (3 * nl) * 96 + 3 * col;
 #pragma unroll
-    for (int m = 0; m < 6; ++m) {
-        const int k = rg + 16 * m, len = (k & ~3) + 4;
+                for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int c4 = 0; c4 < 6; ++c4) {
-            const int col = 24 * cg + 4 * c4;
-            if (col < len) {
-                float4 q = make_float4(v[m][4 * c4], v[m][4 * c4 + 1], v[m][4 * c4 + 2], v[m][4 * c4 + 3]);
-                if (col == (k & ~3)) {  // the diagonal lies in this float4
-                    const int d = k & 3;
-                    q.x = d == 0 ? 1.f : q.x;
-                    q.y = d == 1 ? 1.f : q.y;
-                    q.z = d == 2 ? 1.f : q.z;
-                    q.w = d == 3 ? 1.f : q.w;
-                }
-                *reinterpret_cast<float4*>(&M[m_row(k) + col]) = q;
+                    for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], src[3 * r + c]);
             }
         }
+        __syncthreads();
+    }
+    // CSR terms: lane = (node n = lane % 16, slot group g = lane / 16), ELL slot
+    // k = k0 + g + 4 p; a pass loads 4 slots per lane, then adds them in slot order
+    const int n = lane & 15, g = lane >> 4;
+    const int v = 32 * blk + 16 * H + n;
+    const bool live = v < a.nV;
+    int o = 0, num = 0, base = 0;
+    if (live) {
+        o = a.s2o[v];
+        num = a.nbrNum[v];
+        base = a.ranges[o];
+    }
+    for (int k0 = 0; k0 < a.maxNbr; k0 += 16) {
+        float m[4][9];
+        int col[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int k = k0 + g + 4 * p;
+            col[p] = -1;
+            if (!live || k >= num) continue;
+            if (k == 0) {  // diag (column-major) + additional (row-major), .cpp:1270
+                const float* d = a.diag9 + 9 * (size_t)o;
+                const float* ad = a.additional + 9 * (size_t)v;
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) m[p][r * 3 + c] = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);
+                col[p] = 16 * H + n;
+            } else {
+                const unsigned ot = (unsigned)a.nbr[(size_t)k * a.nV + v];
+                if ((ot >> 5) != ((unsigned)v >> 5)) continue;  // cross-bank: a coarse record
+                const float* src = a.off9 + 9 * ((size_t)base + k - 1);
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) m[p][r * 3 + c] = src[c * 3 + r];
+                col[p] = (int)(ot & 31);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg)  // slot order within the vertex (duplicate neighbours add in ELL order)
+                if (g == gg && col[p] >= 0) {
+                    float* e = S + (3 * n) * 96 + 3 * col[p];
+#pragma unroll
+                    for (int r = 0; r < 3; ++r)
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], m[p][r * 3 + c]);
+                }
     }
     __syncthreads();
-    if (MFMA) form_mfma(M, dinv, inv + blk * kBlockFloats, tileSlot, t);  // one wave: no barrier around M
-    else form_packed_staged(M, dinv, inv + blk * kBlockFloats, valuSlot, t);
+    if (lane < 16) {  // zero diagonal -> identity node block (.cpp:1365-1368)
+        float* e = S + (3 * lane) * 96 + 3 * (16 * H + lane);
+        if (*e == 0.0f)
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) e[r * 96 + c] = (r == c) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (a.keep) {
+        float4* dst = reinterpret_cast<float4*>(a.keep + (size_t)blk * kDenseFloats + 48 * 96 * H);
+        for (int q = lane; q < 48 * 96 / 4; q += 64) dst[q] = S4[q];
+    }
+}
+
+template <int H>
+__device__ __forceinline__ void slab_to_tiles(float (&v)[6][24], const float* S, int lane) {
+    const int rg = lane >> 2, cg = lane & 3;
+#pragma unroll
+    for (int mm = 0; mm < 3; ++mm)
+#pragma unroll
+        for (int c4 = 0; c4 < 6; ++c4) {
+            const float4 q = *reinterpret_cast<const float4*>(&S[(rg + 16 * mm) * 96 + 24 * cg + 4 * c4]);
+            v[3 * H + mm][4 * c4] = q.x;
+            v[3 * H + mm][4 * c4 + 1] = q.y;
+            v[3 * H + mm][4 * c4 + 2] = q.z;
+            v[3 * H + mm][4 * c4 + 3] = q.w;
+        }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_fused(
+    FineAsm a, float* __restrict__ inv, const uint4* __restrict__ valuSlot, int blk0) {
+    static_assert(48 * 96 <= kPackedM, "a slab fits in M's LDS");
+    __shared__ __attribute__((aligned(16))) float M[kPackedM];
+    __shared__ __attribute__((aligned(16))) float piv[96];
+    __shared__ float dinv[96];
+    const int t = threadIdx.x;
+    const int blk = blk0 + blockIdx.x;
+    float v[6][24];
+    build_slab<0>(a, blk, M, t);
+    slab_to_tiles<0>(v, M, t);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab 0 read before slab 1 overwrites it
+    __syncthreads();
+    build_slab<1>(a, blk, M, t);
+    slab_to_tiles<1>(v, M, t);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    factor_tiles<false>(v, M, piv, dinv, inv + (size_t)blk * kBlockFloats, nullptr, valuSlot, t);
+}
+
+int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s) {
+    if (blk1 > blk0)
+        k_factor_fused<<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->valuSlot), blk0);
+    return hip_check(h, hipGetLastError(), "fused factor kernel");
 }
 
 int upload_slot_table(mas_context* h) {
@@ -471,12 +633,12 @@ int copy_block_inverse(mas_context* h, int blk, float* out96) {
 }
 
 int run_factor(mas_context* h, hipStream_t s) {
-    int rc = ensure(h, h->inv, (size_t)h->nBlk * kBlockFloats * 4);
-    if (rc) return rc;
-    float* dense = P<float>(h->dense);
+    float* dense = dense_base(h);
     float* inv = P<float>(h->inv);
-    // the prepared level-0 blocks (all, or a shard's), then every coarse block
-    const int ranges[2][2] = {{h->fineBlk0, h->fineBlk1}, {h->nFineBlk, h->nBlk}};
+    // the prepared level-0 blocks (all, or a shard's; the fused variant factored
+    // them already, on prepStream), then every coarse block
+    const bool fused = h->factorVariant == 4;
+    const int ranges[2][2] = {{h->fineBlk0, fused ? h->fineBlk0 : h->fineBlk1}, {h->nFineBlk, h->nBlk}};
     for (const auto& rg : ranges) {
         const int b0 = rg[0], nb = rg[1] - rg[0];
         if (nb <= 0) continue;
@@ -490,7 +652,9 @@ int run_factor(mas_context* h, hipStream_t s) {
                 k_factor_rb<false><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0);
         }
     }
-    return hip_check(h, hipGetLastError(), "factor kernel");
+    int rc = hip_check(h, hipGetLastError(), "factor kernel");
+    if (!rc && fused) rc = hip_check(h, hipStreamWaitEvent(s, h->evPrepJoin, 0), "join fused factor");
+    return rc;
 }
 
 }  // namespace mas

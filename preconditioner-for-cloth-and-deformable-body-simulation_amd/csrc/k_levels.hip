@@ -180,11 +180,26 @@ __global__ __launch_bounds__(256) void k_connect_lx(int nV, const int* __restric
     }
 }
 
+// Level sizes stay on the device while the levels are built (one host read
+// after the last level): tot[l] = node count of level l >= 1 (written by
+// k_assign_ids of level l - 1), level l starts at id begin_l = nv32 +
+// sum_{1 <= j < l} ceil32(tot[j]).  Grids are sized for the level-0 count.
+__device__ __forceinline__ int level_count(int n0, const int* tot, int level) { return level == 0 ? n0 : tot[level]; }
+__device__ __forceinline__ int level_begin(const int* tot, int level, int nv32) {
+    int b = nv32;
+    for (int j = 1; j < level; ++j) b += (tot[j] + 31) / 32 * 32;
+    return level == 0 ? 0 : b;
+}
+
 // PreparePrefixSumL0 (.cpp:565-628) / NextLevelCluster (.cpp:873-961):
 // per-bank bit-BFS closure from each lane, leader = lowest lane of its mask,
-// leaders counted per bank.
-__global__ __launch_bounds__(256) void k_bank_closure(int n, unsigned* __restrict__ masks, int* __restrict__ counts) {
+// leaders counted per bank; save (levels >= 1 below the top): the closed masks
+// also go to the level's slice of coarseMask (the apply's child lists).
+__global__ __launch_bounds__(256) void k_bank_closure(int n0, const int* __restrict__ tot, int level, int nv32,
+                                                      unsigned* __restrict__ masks, int* __restrict__ counts,
+                                                      unsigned* __restrict__ save) {
     __shared__ unsigned cache[256];
+    const int n = level_count(n0, tot, level);
     const int t = threadIdx.x, lane = t & 31, gbase = t & ~31;
     const int c = blockIdx.x * 256 + t;
     cache[t] = (1u << lane) | (c < n ? masks[c] : 0u);
@@ -200,6 +215,7 @@ __global__ __launch_bounds__(256) void k_bank_closure(int n, unsigned* __restric
             m |= cache[gbase + nxt];
         }
         masks[c] = m;
+        if (save) save[level_begin(tot, level, nv32) - nv32 + c] = m;
         leader = __popc(m & ((1u << lane) - 1u)) == 0;
     }
     unsigned long long b = __ballot(leader);
@@ -208,11 +224,12 @@ __global__ __launch_bounds__(256) void k_bank_closure(int n, unsigned* __restric
 
 // BuildLevel1 (.cpp:630-740) / PrefixSumLx (.cpp:963-1072): cluster id =
 // bank prefix + rank of the lowest lane of the component among the leaders.
-__global__ __launch_bounds__(256) void k_assign_ids(int n, int level, int begin, int nv32,
-                                                    unsigned* __restrict__ masks, const int* __restrict__ prefix,
-                                                    const int* __restrict__ counts, int nBanks,
+__global__ __launch_bounds__(256) void k_assign_ids(int n0, int level, int nv32, unsigned* __restrict__ masks,
+                                                    const int* __restrict__ prefix, const int* __restrict__ counts,
                                                     int* __restrict__ cst0, int* __restrict__ goingNext,
                                                     int* __restrict__ levelTotal) {
+    const int n = level_count(n0, levelTotal, level), begin = level_begin(levelTotal, level, nv32);
+    const int nBanks = (n + 31) / 32;
     const int t = threadIdx.x, lane = t & 31;
     const int c = blockIdx.x * 256 + t;
     unsigned m = c < n ? masks[c] : 0u;
@@ -230,7 +247,7 @@ __global__ __launch_bounds__(256) void k_assign_ids(int n, int level, int begin,
             goingNext[begin + c] = id + begin + ((n + 31) / 32) * 32;
         }
     }
-    if (c == 0) levelTotal[level + 1] = prefix[nBanks - 1] + counts[nBanks - 1];
+    if (c == 0) levelTotal[level + 1] = nBanks ? prefix[nBanks - 1] + counts[nBanks - 1] : 0;
 }
 
 // ComputeNextLevel, .cpp:1074-1084
@@ -269,11 +286,6 @@ static int scan_counts(mas_context* h, const int* counts, int* prefix, int n, hi
     return hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, counts, prefix, n, s), "exclusive scan");
 }
 
-static int read_int(mas_context* h, const int* dptr, int* out, hipStream_t s) {
-    int rc = hip_check(h, hipMemcpyAsync(out, dptr, sizeof(int), hipMemcpyDeviceToHost, s), "D2H level total");
-    if (rc) return rc;
-    return hip_check(h, hipStreamSynchronize(s), "level sync");
-}
 
 // Contact records and their count arrays may live on the host or on the
 // device (e.g. straight from a GPU collision-detection pass):
@@ -370,34 +382,36 @@ int run_levels(mas_context* h, hipStream_t s) {
     // level 0 -> 1
     k_connect_l0<<<g, 256, 0, s>>>(nV, P<int>(h->nbrNumRem), P<int>(h->nbrRem), fine);
     if (h->nStencil) k_collision_connect<<<cdiv(h->nStencil, 256), 256, 0, s>>>(st, h->nStencil, nullptr, fine);
-    k_bank_closure<<<cdiv(nV, 256), 256, 0, s>>>(nV, fine, cnt);
+    k_bank_closure<<<cdiv(nV, 256), 256, 0, s>>>(nV, tot, 0, nv32, fine, cnt, nullptr);
     if ((rc = scan_counts(h, cnt, pre, nB0, s))) return rc;
-    k_assign_ids<<<cdiv(nV, 256), 256, 0, s>>>(nV, 0, 0, nv32, fine, pre, cnt, nB0, cst, gn, tot);
-    int total = 0;
-    if ((rc = read_int(h, tot + 1, &total, s))) return rc;
-    h->levelSize[2] = total;
-    h->levelSize[3] = nv32;
+    k_assign_ids<<<cdiv(nV, 256), 256, 0, s>>>(nV, 0, nv32, fine, pre, cnt, cst, gn, tot);
 
-    for (int level = 1; level < L; ++level) {  // .cpp:427-440
-        const int n = h->levelSize[2 * level], begin = h->levelSize[2 * level + 1];
-        const int nb = cdiv(n, 32);
+    // levels >= 1 (.cpp:427-440): sizes on the device, grids for <= nV nodes
+    // (a level has at most as many nodes as vertices; banks past its count are
+    // never read), no host round trip until the hierarchy is complete
+    for (int level = 1; level < L; ++level) {
         const int* prev = cst + (size_t)(level - 1) * nV;
         if ((rc = hip_check(h, hipMemsetAsync(next, 0, (size_t)nv32 * 4, s), "memset nextMask"))) return rc;
         k_connect_lx<<<g, 256, 0, s>>>(nV, prev, P<int>(h->nbrNumRem), P<int>(h->nbrRem), next);
         if (h->nStencil) k_collision_connect<<<cdiv(h->nStencil, 256), 256, 0, s>>>(st, h->nStencil, prev, next);
-        k_bank_closure<<<cdiv(n, 256), 256, 0, s>>>(n, next, cnt);
-        // keep the level-l component masks (the apply's child lists) before
+        // keeps the level-l component masks (the apply's child lists) before
         // k_assign_ids overwrites them with ids
-        if (level + 1 < L &&
-            (rc = hip_check(h, hipMemcpyAsync(P<unsigned>(h->coarseMask) + (begin - nv32), next, (size_t)n * 4,
-                                              hipMemcpyDeviceToDevice, s), "save masks")))
-            return rc;
-        if ((rc = scan_counts(h, cnt, pre, nb, s))) return rc;
-        k_assign_ids<<<cdiv(n, 256), 256, 0, s>>>(n, level, begin, nv32, next, pre, cnt, nb, nullptr, gn, tot);
+        k_bank_closure<<<cdiv(nV, 256), 256, 0, s>>>(0, tot, level, nv32, next, cnt,
+                                                     level + 1 < L ? P<unsigned>(h->coarseMask) : nullptr);
+        if ((rc = scan_counts(h, cnt, pre, nB0, s))) return rc;
+        k_assign_ids<<<cdiv(nV, 256), 256, 0, s>>>(0, level, nv32, next, pre, cnt, nullptr, gn, tot);
         k_next_level<<<g, 256, 0, s>>>(nV, prev, next, cst + (size_t)level * nV);
-        if ((rc = read_int(h, tot + level + 1, &total, s))) return rc;
-        h->levelSize[2 * (level + 1)] = total;
-        h->levelSize[2 * (level + 1) + 1] = begin + ceil32(n);
+    }
+    int totals[kMaxLevels + 2] = {};
+    if ((rc = hip_check(h, hipMemcpyAsync(totals, tot, (size_t)(L + 1) * 4, hipMemcpyDeviceToHost, s),
+                        "D2H level totals")) ||
+        (rc = hip_check(h, hipStreamSynchronize(s), "level sync")))
+        return rc;
+    h->levelSize[2] = totals[1];
+    h->levelSize[3] = nv32;
+    for (int level = 1; level < L; ++level) {
+        h->levelSize[2 * (level + 1)] = totals[level + 1];
+        h->levelSize[2 * (level + 1) + 1] = h->levelSize[2 * level + 1] + ceil32(totals[level]);
     }
     h->totalClusters = h->levelSize[2 * L + 1];  // TotalNodes, .cpp:1086-1090
     h->nBlk = h->totalClusters / 32;

@@ -105,6 +105,14 @@ int mas_destroy(mas_handle h) {
     if (!h) return MAS_ERR_ARG;
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->prepStream) {
+        hipStreamSynchronize(h->prepStream);
+        hipStreamDestroy(h->prepStream);
+    }
+    if (h->evPrepFork) hipEventDestroy(h->evPrepFork);
+    if (h->evPrepJoin) hipEventDestroy(h->evPrepJoin);
+    for (auto& e : h->evFine)
+        if (e) hipEventDestroy(e);
     h->for_each_buffer([](Buffer& b) { release(b); });
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
@@ -350,9 +358,12 @@ int mas_get_block_matrix(mas_handle h, int blk, float* out96) {
     if (blk < 0 || blk >= h->nBlk) return fail(h, MAS_ERR_ARG, "block index out of range");
     if (blk < h->nFineBlk && (blk < h->fineBlk0 || blk >= h->fineBlk1))
         return fail(h, MAS_ERR_STATE, "level-0 block outside the shard this handle was prepared for");
+    if (blk < h->nFineBlk && !h->denseFine)
+        return fail(h, MAS_ERR_STATE, "level-0 blocks are not stored by the fused assemble + factor "
+                                      "(create the handle with mas_config.keep_blocks = 1)");
     hipSetDevice(h->device);
     hipStreamSynchronize(h->stream);
-    MAS_TRY(hip_check(h, hipMemcpy(out96, P<float>(h->dense) + (size_t)blk * kDenseFloats, kDenseFloats * 4,
+    MAS_TRY(hip_check(h, hipMemcpy(out96, dense_base(h) + (size_t)blk * kDenseFloats, kDenseFloats * 4,
                                    hipMemcpyDeviceToHost), "D2H block"));
     // zero-diagonal -> identity rule (.cpp:1365-1368), as the factor kernel applies it
     for (int x = 0; x < 32; ++x) {

@@ -50,6 +50,27 @@ struct DeepArgs {
     int* cnt;           // per level-3 block: node arrivals (the last one solves the block)
 };
 
+// Level-0 assembly inputs of the fused assemble + factor kernel (k_factor.hip)
+// and the od kernel (k_assemble.hip): the CSR Hessian in the sorted vertex
+// order's ELL neighbour table, the contact rows (`additional`), and the
+// block-entry contact sums of the level-0 blocks, one prefolded 3x3 per
+// distinct entry key at the position its run starts in the sorted records.
+struct FineAsm {
+    int nV, maxNbr;
+    const int* s2o;
+    const int* nbrNum;
+    const int* nbr;
+    const float* diag9;
+    const float* off9;
+    const int* ranges;
+    const float* additional;
+    const unsigned long long* ckeys;  // sorted block-entry keys (row << B) | col (null: no contacts)
+    const float* cval;                // row-major 3x3 per run start
+    const int* coff;                  // per level-0 block: first record (nFineBlk + 1)
+    int B;
+    float* keep;                      // dense base: also store the assembled blocks (null: not kept)
+};
+
 struct Buffer {
     void* p = nullptr;
     size_t bytes = 0;
@@ -86,7 +107,11 @@ struct mas_context {
     int allocCalls = 0;   // reference m_frameIndex semantics (B-1)
     bool allocated = false, prepared = false, profiling = false;
     bool fromBlob = false;  // restored by mas_load_blob: applies, no Prepare inputs (blob.hip)
-    int factorVariant = 2;  // 2 = register-blocked k_factor_rb; env MAS_FACTOR_VARIANT=0: LDS-row k_factor
+    // level-0 factor (env MAS_FACTOR_VARIANT): 4 = k_factor_fused (assembly in
+    // LDS slabs + register-blocked factor, one kernel, overlapped with the
+    // coarse assembly on prepStream); 2 = k_level0_block + k_factor_rb;
+    // 3 = 2 with the MFMA formation (not bitwise); 0 = LDS-row k_factor
+    int factorVariant = 4;
     // coarse levels (env MAS_COARSE_MODE): 2 = two launches, restrictions then
     // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (One-launch
     // forms and the side-stream overlap were measured slower: DESIGN.md
@@ -109,7 +134,15 @@ struct mas_context {
     mas::Buffer rawContacts, stencilFlags, stencilSlots, stencils;
     mas::Buffer fineMask, nextMask, bankCount, bankPrefix, levelTotal;
     mas::Buffer cst, goingNext, vmap, coarseTables;
+    // dense: the assembled 96x96 blocks.  Only the coarse blocks are stored
+    // unless level-0 blocks are kept (cfg.keep_blocks or an unfused factor
+    // variant); denseBase = the address block 0 would have (dense_base()).
     mas::Buffer dense, inv, slotTable, tileSlot, valuSlot;
+    bool denseFine = false;  // the last Prepare stored the level-0 blocks
+    mas::Buffer cFineVal;    // prefolded level-0 contact entries (FineAsm::cval)
+    hipStream_t prepStream = nullptr;  // fused level-0 assemble + factor, beside the coarse assembly
+    hipEvent_t evPrepFork = nullptr, evPrepJoin = nullptr;
+    hipEvent_t evFine[2] = {nullptr, nullptr};  // timing of the fused level-0 kernel (prepare_fine_ms)
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
     // contact records (k_assemble.hip): block entries (d*), additional rows (a*), pushes (p*)
@@ -159,7 +192,7 @@ struct mas_context {
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &tileSlot, &valuSlot, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
                               &vlist, &voff, &tab, &termCnt, &termOff, &terms,
-                              &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &caCnt, &caOff,
+                              &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cFineVal, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
                               &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
@@ -179,6 +212,10 @@ template <class T>
 inline const T* P(const Buffer& b) { return reinterpret_cast<const T*>(b.p); }
 inline int ceil32(int x) { return (x + 31) / 32 * 32; }
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+// block b's 96x96 at dense_base(h) + 9216 b (b >= nFineBlk unless denseFine)
+inline float* dense_base(mas_context* h) {
+    return P<float>(h->dense) - (h->denseFine ? 0 : (ptrdiff_t)h->nFineBlk * kDenseFloats);
+}
 
 // phase entry points (host orchestration), defined per translation unit
 int run_allocate(mas_context* h, const float* pos4, const int* starts, const int* idx, const int* edges4,
@@ -191,6 +228,8 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
 int run_levels(mas_context* h, hipStream_t s);
 int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s);
 int run_factor(mas_context* h, hipStream_t s);
+// fused level-0 assemble + factor of blocks [blk0, blk1) (k_factor.hip)
+int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s);
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s);
 int upload_slot_table(mas_context* h);
 int prepare_apply_tables(mas_context* h, hipStream_t s);

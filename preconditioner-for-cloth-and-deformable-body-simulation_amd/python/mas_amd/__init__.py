@@ -46,7 +46,7 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
 
 class mas_config(ctypes.Structure):
     _fields_ = [("max_levels", ctypes.c_int), ("resort_period", ctypes.c_int), ("fix_vf_bary", ctypes.c_int),
-                ("device", ctypes.c_int), ("reserved", ctypes.c_int * 12)]
+                ("device", ctypes.c_int), ("keep_blocks", ctypes.c_int), ("reserved", ctypes.c_int * 11)]
 
 
 class mas_info(ctypes.Structure):
@@ -62,7 +62,7 @@ class mas_stats(ctypes.Structure):
                                                "prepare_assemble_ms", "prepare_factor_ms")] + \
                [("apply_calls", ctypes.c_int64), ("profiled_applies", ctypes.c_int64)] + \
                [(n, ctypes.c_double) for n in ("apply_ms_avg", "pre_fine_ms_avg", "fine_ms_avg", "post_fine_ms_avg")] + \
-               [("apply_mode", ctypes.c_int64)]
+               [("apply_mode", ctypes.c_int64), ("prepare_fine_ms", ctypes.c_double)]
 
 
 class mas_shard(ctypes.Structure):
@@ -195,9 +195,10 @@ def _dev(t, count, width, dtype_name, name):
 class SeSchwarzPreconditioner:
     """Reference-compatible surface (SE::SeSchwarzPreconditioner) on the GPU."""
 
-    def __init__(self, max_levels: int = 0, resort_period: int = 0, fix_vf_bary: bool = False, device: int = -1):
+    def __init__(self, max_levels: int = 0, resort_period: int = 0, fix_vf_bary: bool = False, device: int = -1,
+                 keep_blocks: bool = False):
         self._L = lib()
-        cfg = mas_config(max_levels, resort_period, int(fix_vf_bary), device)
+        cfg = mas_config(max_levels, resort_period, int(fix_vf_bary), device, int(bool(keep_blocks)))
         h = ctypes.c_void_p()
         rc = self._L.mas_create(ctypes.byref(h), ctypes.byref(cfg))
         if rc != MAS_OK:

@@ -1,0 +1,26 @@
+"""Prepare-only driver for profiling: one config, N steady-state Prepares.
+python scripts/dev/prep_only.py [config] [reps]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "../../preconditioner-for-cloth-and-deformable-body-simulation_amd/python"))
+
+import mas_amd
+from mas_amd import meshgen
+
+cfg_name = sys.argv[1] if len(sys.argv) > 1 else "1M+contacts"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+mesh, cfg = meshgen.build_config(cfg_name)
+contacts = meshgen.vf_contacts(mesh, cfg["contacts"], seed=3) if cfg["contacts"] else None
+P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts)
+for _ in range(reps):
+    t0 = time.perf_counter()
+    if contacts is None:
+        P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
+    else:
+        P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, contacts[0], None, None, contacts[1])
+    st = P.stats()
+    print(f"prepare {st['prepare_ms']:.3f} ms (levels {st['prepare_levels_ms']:.3f}, assemble "
+          f"{st['prepare_assemble_ms']:.3f}, factor {st['prepare_factor_ms']:.3f}, fused level-0 {st['prepare_fine_ms']:.3f}); host {1e3*(time.perf_counter()-t0):.1f} ms",
+          flush=True)

@@ -71,7 +71,7 @@ SMALL = [("cloth", 20, 0), ("cloth", 40, 0), ("cloth", 64, 0), ("cloth", 100, 0)
 def test_small_configs_parity(kind, W, L):
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
-    P = _gpu(mesh, L)
+    P = _gpu(mesh, L, keep_blocks=True)  # level-0 blocks stored for block_matrix
     o = _oracle(mesh, L)
     compare_maps(P, o, mesh.nV)
     info = P.info()
@@ -149,10 +149,11 @@ def test_1m_cloth_parity():
 
 
 def test_1m_contacts_parity():
+    import mas_amd
     from mas_amd import meshgen
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    P = _gpu(mesh, 4, contacts=contacts)
+    P = _gpu(mesh, 4, contacts=contacts, keep_blocks=True)
     o = _oracle(mesh, 4, contacts=contacts, threads=8)
     assert P.info()["num_stencils"] == o.num_stencils == 100_000
     compare_maps(P, o, mesh.nV)
@@ -169,13 +170,23 @@ def test_1m_contacts_parity():
     P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, contacts[0], None, None, contacts[1])
     np.testing.assert_array_equal(P.save_blob(), blob)
     np.testing.assert_array_equal(P.Preconditioning(None, r), z1)
+    # the default handle (fused level-0 assemble + factor, blocks not stored):
+    # the same inverses and z, and level-0 block matrices refused
+    Pd = _gpu(mesh, 4, contacts=contacts)
+    np.testing.assert_array_equal(Pd.save_blob(), blob)
+    with pytest.raises(mas_amd.MasError, match="STATE"):
+        Pd.block_matrix(0)
+    np.testing.assert_array_equal(Pd.block_matrix(nfine), P.block_matrix(nfine))
 
 
-@pytest.mark.parametrize("kind,W,L,nc", [("cloth", 100, 0, 300), ("tet", 16, 3, 0), ("cloth", 33, 0, 0)])
+@pytest.mark.parametrize("kind,W,L,nc", [("cloth", 100, 0, 300), ("tet", 16, 3, 0), ("cloth", 33, 0, 0),
+                                         ("cloth", 128, 4, 3000), ("tet", 12, 0, 0)])
 def test_factor_kernels_agree_bitwise(kind, W, L, nc, monkeypatch):
-    """k_factor (LDS rows, MAS_FACTOR_VARIANT=0) and k_factor_rb (register
-    tiles, default) run the reference's operations in the reference's order:
-    every block inverse (fine and coarse, with padding nodes) must be equal."""
+    """k_factor (LDS rows, MAS_FACTOR_VARIANT=0), k_level0_block + k_factor_rb
+    (register tiles, 2) and k_factor_fused (assembly in LDS slabs + register
+    tiles, the default 4) run the reference's operations in the reference's
+    order: every block inverse (fine and coarse, with padding nodes) and every
+    stored block must be equal."""
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=5) if nc else None
@@ -183,11 +194,19 @@ def test_factor_kernels_agree_bitwise(kind, W, L, nc, monkeypatch):
     P0 = _gpu(mesh, L, contacts=contacts)
     monkeypatch.setenv("MAS_FACTOR_VARIANT", "2")
     P2 = _gpu(mesh, L, contacts=contacts)
+    monkeypatch.delenv("MAS_FACTOR_VARIANT")
+    P4 = _gpu(mesh, L, contacts=contacts)
+    P4k = _gpu(mesh, L, contacts=contacts, keep_blocks=True)
     nb = P0.info()["num_blocks"]
     for blk in range(nb):
         np.testing.assert_array_equal(P2.block_inverse(blk), P0.block_inverse(blk))
+        np.testing.assert_array_equal(P4.block_inverse(blk), P0.block_inverse(blk), err_msg=str(blk))
+        np.testing.assert_array_equal(P4k.block_matrix(blk), P2.block_matrix(blk), err_msg=str(blk))
+    np.testing.assert_array_equal(P4k.save_blob(), P4.save_blob())
     r = meshgen.residual(mesh.nV, 17)
-    np.testing.assert_array_equal(P2.Preconditioning(None, r), P0.Preconditioning(None, r))
+    z0 = P0.Preconditioning(None, r)
+    np.testing.assert_array_equal(P2.Preconditioning(None, r), z0)
+    np.testing.assert_array_equal(P4.Preconditioning(None, r), z0)
 
 
 @pytest.mark.parametrize("W,L,n", [(64, 0, 300), (100, 3, 1000), (128, 4, 3000)])
@@ -202,7 +221,7 @@ def test_all_contact_types_parity(W, L, n):
     ef, efC = meshgen.ef_contacts(mesh, n)
     ee, eeC = meshgen.ee_contacts(mesh, n)
     vf, vfC = meshgen.vf_contacts(mesh, n)
-    P = mas_amd.SeSchwarzPreconditioner(max_levels=L)
+    P = mas_amd.SeSchwarzPreconditioner(max_levels=L, keep_blocks=True)
     P.m_positions, P.m_neighbours, P.m_edges, P.m_faces = mesh.pos, (mesh.starts, mesh.idx), mesh.edges, mesh.faces
     P.AllocatePrecoditioner(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0])
     P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, ef, ee, vf, efC, eeC, vfC)

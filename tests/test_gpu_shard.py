@@ -76,7 +76,8 @@ def test_shard_prepared_handles_bitwise(kind, W, L, world, nc):
     """Sharded Prepare (mas_set_prepare_shard): rank g's handle
     assembles and factors only its own level-0 blocks (plus the replicated
     coarse levels); its restrict and finish reproduce the unsharded apply's z
-    on its vertices bit for bit, and its factor phase shrinks with the world.
+    on its vertices bit for bit, and its level-0 assemble + factor time
+    (prepare_fine_ms) shrinks with the world.
     Such a handle refuses the single-GPU apply, other shards and other ranks'
     level-0 blocks.  Includes BASELINE configs[3] (1M + 100k VF contacts) and
     configs[4] (4M tet lattice) at 8 ranks."""
@@ -88,7 +89,7 @@ def test_shard_prepared_handles_bitwise(kind, W, L, world, nc):
     Pf = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
     r = torch.from_numpy(meshgen.residual(mesh.nV, 6)).cuda()
     z_ref = _unsharded(Pf, r)
-    t_full = Pf.stats()["prepare_factor_ms"]
+    t_full = Pf.stats()["prepare_fine_ms"]
     ranks = [mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, shard=(g, world)) for g in range(world)]
     s = torch.cuda.Stream()
     plans = [Pg.shard_setup(g, world) for g, Pg in enumerate(ranks)]
@@ -103,8 +104,8 @@ def test_shard_prepared_handles_bitwise(kind, W, L, world, nc):
             Pg.shard_finish(g, world, gathered, r, z, s.cuda_stream)
     s.synchronize()
     assert torch.equal(z, z_ref), float((z - z_ref).abs().max())
-    t_rank = max(Pg.stats()["prepare_factor_ms"] for Pg in ranks)
-    print(f"factor phase: unsharded {t_full:.3f} ms, slowest of {world} ranks {t_rank:.3f} ms")
+    t_rank = max(Pg.stats()["prepare_fine_ms"] for Pg in ranks)
+    print(f"level-0 assemble + factor: unsharded {t_full:.3f} ms, slowest of {world} ranks {t_rank:.3f} ms")
     if mesh.nV >= 1_000_000:
         assert t_rank < 0.35 * t_full, (t_rank, t_full)
     P1 = ranks[1]
@@ -151,16 +152,6 @@ def test_sharded_apply_helper_overlap_world1():
         S(z, r, s)
         s.synchronize()
         assert np.array_equal(z.cpu().numpy(), P.Preconditioning(None, r.cpu().numpy())), overlap
-
-
-def _unsharded(P, r):
-    import torch
-    z = torch.zeros_like(r)
-    torch.cuda.synchronize()
-    s = torch.cuda.Stream()
-    P.PreconditioningDevice(z, r, s.cuda_stream)
-    s.synchronize()
-    return z
 
 
 @pytest.mark.parametrize("kind,W,L,worlds,nc", [("cloth", 100, 3, (1, 2, 3), 0), ("tet", 16, 3, (2, 8), 0),
