@@ -910,7 +910,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         return rc;
     fc = FineContacts{P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
                       B};
-    if (h->factorVariant == 4) {
+    if (h->factorVariant >= 4) {
         if (fineEnd > 0) {
             // each level-0 entry's contact run folded from zero once, stored at
             // the run's first position (the fused kernel adds it to its zero entry)
@@ -953,7 +953,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
 int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s) {
     const int nV = h->nV, L = h->L, tc = h->totalClusters;
     int rc;
-    const bool fused = h->factorVariant == 4;
+    const bool fused = h->factorVariant >= 4;
     // the fused factor never stores level-0 blocks unless asked to keep them
     h->denseFine = !fused || h->cfg.keep_blocks;
     const int nStored = h->denseFine ? h->nBlk : h->nBlk - h->nFineBlk;

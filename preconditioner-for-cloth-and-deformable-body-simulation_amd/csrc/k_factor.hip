@@ -552,8 +552,10 @@ __device__ __forceinline__ void slab_to_tiles(float (&v)[6][24], const float* S,
         }
 }
 
+template <bool MFMA>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_fused(
-    FineAsm a, float* __restrict__ inv, const uint4* __restrict__ valuSlot, int blk0) {
+    FineAsm a, float* __restrict__ inv, const uint4* __restrict__ tileSlot, const uint4* __restrict__ valuSlot,
+    int blk0) {
     static_assert(48 * 96 <= kPackedM, "a slab fits in M's LDS");
     __shared__ __attribute__((aligned(16))) float M[kPackedM];
     __shared__ __attribute__((aligned(16))) float piv[96];
@@ -569,12 +571,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     slab_to_tiles<1>(v, M, t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    factor_tiles<false>(v, M, piv, dinv, inv + (size_t)blk * kBlockFloats, nullptr, valuSlot, t);
+    factor_tiles<MFMA>(v, M, piv, dinv, inv + (size_t)blk * kBlockFloats, tileSlot, valuSlot, t);
 }
 
 int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s) {
-    if (blk1 > blk0)
-        k_factor_fused<<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->valuSlot), blk0);
+    // MAS_FACTOR_VARIANT=5: the matrix-core formation (form_mfma, not bitwise)
+    if (blk1 > blk0 && h->factorVariant == 5)
+        k_factor_fused<true><<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
+                                                        P<uint4>(h->valuSlot), blk0);
+    else if (blk1 > blk0)
+        k_factor_fused<false><<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
+                                                         P<uint4>(h->valuSlot), blk0);
     return hip_check(h, hipGetLastError(), "fused factor kernel");
 }
 
@@ -637,7 +644,7 @@ int run_factor(mas_context* h, hipStream_t s) {
     float* inv = P<float>(h->inv);
     // the prepared level-0 blocks (all, or a shard's; the fused variant factored
     // them already, on prepStream), then every coarse block
-    const bool fused = h->factorVariant == 4;
+    const bool fused = h->factorVariant >= 4;
     const int ranges[2][2] = {{h->fineBlk0, fused ? h->fineBlk0 : h->fineBlk1}, {h->nFineBlk, h->nBlk}};
     for (const auto& rg : ranges) {
         const int b0 = rg[0], nb = rg[1] - rg[0];

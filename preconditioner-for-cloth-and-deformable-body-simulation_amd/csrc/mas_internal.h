@@ -110,7 +110,8 @@ struct mas_context {
     // level-0 factor (env MAS_FACTOR_VARIANT): 4 = k_factor_fused (assembly in
     // LDS slabs + register-blocked factor, one kernel, overlapped with the
     // coarse assembly on prepStream); 2 = k_level0_block + k_factor_rb;
-    // 3 = 2 with the MFMA formation (not bitwise); 0 = LDS-row k_factor
+    // 3 = 2 with the MFMA formation (not bitwise); 5 = 4 with the MFMA
+    // formation (not bitwise); 0 = LDS-row k_factor
     int factorVariant = 4;
     // coarse levels (env MAS_COARSE_MODE): 2 = two launches, restrictions then
     // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (One-launch

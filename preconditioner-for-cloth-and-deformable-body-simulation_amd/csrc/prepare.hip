@@ -52,7 +52,7 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     h->stats.prepare_assemble_ms = b;
     h->stats.prepare_factor_ms = c;
     float f = 0;
-    if (h->factorVariant == 4 && h->evFine[0]) hipEventElapsedTime(&f, h->evFine[0], h->evFine[1]);
+    if (h->factorVariant >= 4 && h->evFine[0]) hipEventElapsedTime(&f, h->evFine[0], h->evFine[1]);
     h->stats.prepare_fine_ms = f;
     h->prepared = true;
     return MAS_OK;

@@ -1,6 +1,6 @@
-"""The matrix-core inverse formation (MAS_FACTOR_VARIANT=3, k_factor.hip
-form_mfma) against the reference-order VALU formation (the default, bitwise
-equal to the oracle for equal blocks).
+"""The matrix-core inverse formation (k_factor.hip form_mfma: MAS_FACTOR_VARIANT
+3 = unfused, 5 = inside the fused level-0 kernel) against the reference-order
+VALU formation (the default, bitwise equal to the oracle for equal blocks).
 
 The elimination is shared, so the two differ only in the order in which the
 96 products of every inverse entry are summed.  Bars: every block's inverse
@@ -15,21 +15,22 @@ from conftest import cloth, tet
 pytestmark = pytest.mark.gpu
 
 
-def _pair(mesh, L, contacts, monkeypatch):
+def _pair(mesh, L, contacts, monkeypatch, variant):
     import mas_amd
     monkeypatch.setenv("MAS_FACTOR_VARIANT", "2")
     P2 = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
-    monkeypatch.setenv("MAS_FACTOR_VARIANT", "3")
+    monkeypatch.setenv("MAS_FACTOR_VARIANT", variant)
     P3 = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
     return P2, P3
 
 
+@pytest.mark.parametrize("variant", ["3", "5"])
 @pytest.mark.parametrize("kind,W,L,nc", [("cloth", 64, 0, 200), ("tet", 16, 3, 0), ("cloth", 33, 0, 0)])
-def test_mfma_inverse_matches_valu(kind, W, L, nc, monkeypatch):
+def test_mfma_inverse_matches_valu(kind, W, L, nc, variant, monkeypatch):
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=5) if nc else None
-    P2, P3 = _pair(mesh, L, contacts, monkeypatch)
+    P2, P3 = _pair(mesh, L, contacts, monkeypatch, variant)
     worst = 0.0
     for blk in range(P2.info()["num_blocks"]):
         a, b = P2.block_inverse(blk), P3.block_inverse(blk)
@@ -39,12 +40,13 @@ def test_mfma_inverse_matches_valu(kind, W, L, nc, monkeypatch):
     assert worst <= 2e-5, worst
 
 
-def test_mfma_z_within_tolerance_1m_contacts(monkeypatch):
+@pytest.mark.parametrize("variant", ["3", "5"])
+def test_mfma_z_within_tolerance_1m_contacts(variant, monkeypatch):
     from mas_amd import meshgen
     from oracle import Oracle
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    monkeypatch.setenv("MAS_FACTOR_VARIANT", "3")
+    monkeypatch.setenv("MAS_FACTOR_VARIANT", variant)
     import mas_amd
     P3 = mas_amd.from_mesh(mesh, max_levels=4, contacts=contacts)
     o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], 4, 8)
