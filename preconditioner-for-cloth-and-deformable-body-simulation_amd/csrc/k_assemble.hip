@@ -34,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 #include <type_traits>
@@ -811,24 +812,13 @@ int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const in
 
 // Fused variant: k_factor_fused over the prepared level-0 blocks on
 // prepStream, after everything this stream has queued (its inputs: additional
-// and the prefolded level-0 contact entries); run_factor joins.  With
-// MAS_PREP_CU_RESERVE=k the side stream leaves k CUs to the coarse assembly
-// (a CU-masked queue), which otherwise waits for the fused kernel's slots.
+// and the prefolded level-0 contact entries); run_factor joins
+// (measured: a CU-masked side stream, stream priorities and a persistent
+// fused grid all lost to this plain form).
 static int fork_fused(mas_context* h, const FineAsm& fa, hipStream_t s) {
     int rc;
     if (!h->prepStream) {
-        int reserve = 0;
-        if (const char* e = std::getenv("MAS_PREP_CU_RESERVE")) reserve = std::atoi(e);
-        hipDeviceProp_t prop{};
-        if (reserve > 0 && hipGetDeviceProperties(&prop, h->device) == hipSuccess &&
-            reserve < prop.multiProcessorCount) {
-            const int n = prop.multiProcessorCount, words = (n + 31) / 32;
-            std::vector<uint32_t> mask(words, 0);
-            for (int cu = 0; cu < n - reserve; ++cu) mask[cu / 32] |= 1u << (cu % 32);
-            rc = hip_check(h, hipExtStreamCreateWithCUMask(&h->prepStream, words, mask.data()), "prepare stream");
-        } else {
-            rc = hip_check(h, hipStreamCreateWithFlags(&h->prepStream, hipStreamNonBlocking), "prepare stream");
-        }
+        rc = hip_check(h, hipStreamCreateWithFlags(&h->prepStream, hipStreamNonBlocking), "prepare stream");
         if (rc || (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepFork, hipEventDisableTiming), "event")) ||
             (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepJoin, hipEventDisableTiming), "event")) ||
             (rc = hip_check(h, hipEventCreate(&h->evFine[0]), "event")) ||
