@@ -27,9 +27,10 @@
 // adding +0.0 to a fold that starts at +0 is exact), so a node's values are
 // one contiguous run at a position known without a load: the workgroup loads
 // it coalesced into LDS and lanes 0..2 fold x, y, z.  The node's R is
-// published through a release/acquire arrival counter per block; the block's
-// last arriver solves it (its wave 1 prefetched the inverse) and resets the
-// counter for the next apply.
+// published with write-through stores and a relaxed agent-scope arrival
+// counter per block (an acq_rel atomic measured 4.8 us); the block's last
+// arriver reads the others' R with sc1 loads, solves the block (its wave 1
+// prefetched the inverse) and resets the counter for the next apply.
 // Levels >= 4 (L = 5) are not computed: CollectFinalZ prolongs only levels
 // 1..3 (.cpp:1706-1717, B-6), so the reference's R4/Z4 never reach z; folding
 // them in its order would be a chain over every level-1 node (n1 adds).
@@ -175,6 +176,12 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve123(const float4* __rest
         deep_node<false>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, q.begin1);
         return;
     }
+    // The level-1/2 solves have slack (~4 us of work beside the ~11 us
+    // level-3 chain): held back ~1.7 us (s_sleep 64 x 64 cycles), their 20 MB
+    // of inverse loads no longer queue in front of the deep lists and the
+    // fold's SIMDs stay quiet.  pre-fine 21.7 -> 19.4 us at 1M + contacts
+    // (sleep 32 / 64 / 127: 19.9 / 19.4 / 19.9 us).
+    if (q.nDeepNodes > 0) __builtin_amdgcn_s_sleep(64);
     const int lane = threadIdx.x & 63, n = lane & 31;
     const int w = (blockIdx.x - q.nDeepNodes) * (kApplyThreads / 64) + (threadIdx.x >> 6);
     [[maybe_unused]] const int pw = blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -100,6 +100,9 @@ __global__ __launch_bounds__(kApplyThreads) void k_shard_coarse12(
         deep_node<true>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, begin1);
         return;
     }
+    // the level-1/2 waves have slack: held back as in k_solve123 (one-rank
+    // sharded complete 31.0-31.5 -> 30.5-30.8 us)
+    if (nDeep > 0) __builtin_amdgcn_s_sleep(64);
     const int lane = threadIdx.x & 63, n = lane & 31;
     const int w = (blockIdx.x - nDeep) * (kApplyThreads / 64) + (threadIdx.x >> 6);
     if (w >= nOwn1 + nb2) return;  // wave-uniform
