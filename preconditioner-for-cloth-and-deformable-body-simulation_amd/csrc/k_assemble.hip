@@ -133,9 +133,10 @@ __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restr
 }
 
 // The records of stencil i at dOff[i] / aOff[i], in the reference's order;
-// keys: block entry (my << B) | ot, additional node id.
+// keys: block entry my * 32 + (ot & 31) (RecKey with begin1 = 0: the pair
+// shares a bank at its level), additional node id.
 __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restrict__ st, int n,
-                                                       const int* __restrict__ gn, int L, int B,
+                                                       const int* __restrict__ gn, int L,
                                                        const int* __restrict__ dOff, const int* __restrict__ aOff,
                                                        unsigned long long* __restrict__ dKeys, int* __restrict__ dIds,
                                                        float* __restrict__ dVal, unsigned* __restrict__ aKeys,
@@ -161,8 +162,8 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
             float t[9];
             for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e]);
             // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot]
-            dKeys[d] = ((unsigned long long)my << B) | ot;
-            dKeys[d + 1] = ((unsigned long long)ot << B) | my;
+            dKeys[d] = ((unsigned long long)my << 5) | (ot & 31u);
+            dKeys[d + 1] = ((unsigned long long)ot << 5) | (my & 31u);
             dIds[d] = d;
             dIds[d + 1] = d + 1;
             for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(256) void k_push_write(int nA, int begin1, int tc, 
 // component e of every entry -- the reference adds PrepareCollisionHessian's
 // terms before PrepareHessian's (.cpp:88-97).
 struct FineContacts {
-    const unsigned long long* keys;  // sorted block-entry keys (row << B) | col
+    const unsigned long long* keys;  // sorted block-entry keys row * 32 + (col & 31) (RecKey)
     const int* ids;                  // record index -> 9 column-major floats in val
     const float* val;
     const int* off;                  // per level-0 block: first record (nFineBlk + 1)
@@ -385,18 +386,23 @@ __global__ __launch_bounds__(256) void k_od(FineAsm a, float* __restrict__ od, i
     recCnt[v] = cnt;
 }
 
-// Record keys pack (row, col) as coarse ids relative to level 1 in B bits each
-// (B = bit width of the coarse node count, 16 at 1M): the stable radix sort
-// then runs over 2B bits instead of 64 (4 passes instead of 8 at 1M).  A dead
-// record's key has all 2B bits set, above every live key (ids < 2^B - 1).
+// Entry keys.  A record's row and column nodes always share a bank (the
+// climb stops at the first level where they do), so an entry is its row id
+// relative to begin1 and the column's lane: key = (row - begin1) * 32 +
+// (col & 31), B + 5 bits (B = bit width of the node count above begin1: 16 at
+// 1M, 18 at 4M) instead of 2B -- the stable radix sort runs 3 passes instead
+// of 4 (1M) and 5 (4M).  A dead record's key has all B + 5 bits set, above
+// every live key.  Contact block entries use the same form with begin1 = 0.
 struct RecKey {
     int begin1, B;
-    __device__ unsigned long long dead() const { return (1ull << (2 * B)) - 1; }
+    static constexpr int kLaneBits = 5;
+    __host__ __device__ int bits() const { return B + kLaneBits; }
+    __host__ __device__ unsigned long long dead() const { return (1ull << bits()) - 1; }
     __device__ unsigned long long pack(unsigned row, unsigned col) const {
-        return ((unsigned long long)(row - begin1) << B) | (col - begin1);
+        return ((unsigned long long)(row - begin1) << kLaneBits) | (col & 31u);
     }
-    __device__ unsigned row(unsigned long long k) const { return (unsigned)(k >> B) + begin1; }
-    __device__ unsigned col(unsigned long long k) const { return (unsigned)(k & ((1ull << B) - 1)) + begin1; }
+    __device__ unsigned row(unsigned long long k) const { return (unsigned)(k >> kLaneBits) + begin1; }
+    __device__ unsigned col(unsigned long long k) const { return (row(k) & ~31u) | (unsigned)(k & 31u); }
 };
 
 // one thread per vertex (neighbour counts <= 8: a 2-D cloth has ~2 cross-bank
@@ -870,18 +876,18 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         (rc = ensure(h, h->caIdsS, a1 * 4)) || (rc = ensure(h, h->caVal, a1 * 36)) ||
         (rc = ensure(h, h->cpCnt, (a1 + 1) * 4)) || (rc = ensure(h, h->cpOff, (a1 + 1) * 4)))
         return rc;
-    k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, gn, L, B, P<int>(h->cdOff), P<int>(h->caOff),
+    k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdOff), P<int>(h->caOff),
                                                  P<unsigned long long>(h->cdKeys), P<int>(h->cdIds),
                                                  P<float>(h->cdVal), P<unsigned>(h->caKeys), P<int>(h->caIds),
                                                  P<float>(h->caVal));
     if ((rc = sort_pairs(h, P<unsigned long long>(h->cdKeys), P<unsigned long long>(h->cdKeysS), P<int>(h->cdIds),
-                         P<int>(h->cdIdsS), nD, 2 * B, s, "contact entry sort")) ||
+                         P<int>(h->cdIdsS), nD, B + RecKey::kLaneBits, s, "contact entry sort")) ||
         (rc = sort_pairs(h, P<unsigned>(h->caKeys), P<unsigned>(h->caKeysS), P<int>(h->caIds), P<int>(h->caIdsS), nA,
                          B, s, "contact row sort")))
         return rc;
     float* dense = dense_base(h);
     // fine entries: k_level0_block; coarse entries: folded onto the zeroed coarse blocks
-    k_contact_fine_bounds<<<cdiv(nD + 1, 256), 256, 0, s>>>(nD, B, begin1, h->nFineBlk,
+    k_contact_fine_bounds<<<cdiv(nD + 1, 256), 256, 0, s>>>(nD, RecKey::kLaneBits, begin1, h->nFineBlk,
                                                             P<unsigned long long>(h->cdKeysS), P<int>(h->cFineOff));
     int fineEnd = 0;
     if ((rc = hip_check(h, hipMemcpyAsync(&fineEnd, P<int>(h->cFineOff) + h->nFineBlk, 4, hipMemcpyDeviceToHost, s),
@@ -899,7 +905,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         (rc = hip_check(h, hipStreamSynchronize(s), "push count sync")))
         return rc;
     fc = FineContacts{P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
-                      B};
+                      RecKey::kLaneBits};
     if (h->factorVariant >= 4) {
         if (fineEnd > 0) {
             // each level-0 entry's contact run folded from zero once, stored at
@@ -913,7 +919,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
             fa.ckeys = P<unsigned long long>(h->cdKeysS);
             fa.cval = P<float>(h->cFineVal);
             fa.coff = P<int>(h->cFineOff);
-            fa.B = B;
+            fa.B = RecKey::kLaneBits;
         }
         // the level-0 blocks need nothing below: they start now
         if ((rc = fork_fused(h, fa, s))) return rc;
@@ -1023,10 +1029,10 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     }
     if (nRec > 0) {
         if ((rc = sort_pairs(h, P<unsigned long long>(h->recKeys), P<unsigned long long>(h->recKeysSorted),
-                             P<int>(h->recIds), P<int>(h->recIdsSorted), nRec, 2 * rk.B, s, "record sort")))
+                             P<int>(h->recIds), P<int>(h->recIdsSorted), nRec, rk.bits(), s, "record sort")))
             return rc;
         k_fold_runs<DenseEntry, true, unsigned long long><<<cdiv(nRec, 64), 64, 0, s>>>(
-            nRec, (1ull << (2 * rk.B)) - 1, P<unsigned long long>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
+            nRec, rk.dead(), P<unsigned long long>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
             DenseEntry{dense, rk});
     }
     k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
