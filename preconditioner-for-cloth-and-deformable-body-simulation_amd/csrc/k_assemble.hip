@@ -495,21 +495,33 @@ struct DenseEntry {  // block entry (row node, column node) of the dense buffer
     float* dense;
     RecKey rk;
     static constexpr int kStride = 96;
+    static constexpr bool kFromZero = false;
+    __device__ bool live(unsigned long long) const { return true; }
     __device__ float* at(unsigned long long k, int) const { return entry(dense, rk.row(k), rk.col(k)); }
 };
 struct DenseDiag {  // the diagonal entry of a node
     float* dense;
     static constexpr int kStride = 96;
+    static constexpr bool kFromZero = false;
+    __device__ bool live(unsigned) const { return true; }
     __device__ float* at(unsigned k, int) const { return entry(dense, k, k); }
 };
 struct NodeRow {  // a row-major 9-float row per node (additional)
     float* base;
     static constexpr int kStride = 3;
+    static constexpr bool kFromZero = false;
+    __device__ bool live(unsigned) const { return true; }
     __device__ float* at(unsigned k, int) const { return base + 9 * (size_t)k; }
 };
-struct RunSlot {  // a row-major 3x3 per run, at the run's first sorted position (FineAsm::cval)
+// a row-major 3x3 per level-0 entry run (row < begin1), folded from zero and
+// stored at the run's first sorted position (FineAsm::cval): no memset, and
+// launched over all records so the host needs no count (coarse runs skipped)
+struct RunSlot {
     float* base;
+    unsigned begin1;
     static constexpr int kStride = 3;
+    static constexpr bool kFromZero = true;
+    __device__ bool live(unsigned long long k) const { return (k >> RecKey::kLaneBits) < begin1; }
     __device__ float* at(unsigned long long, int start) const { return base + 9 * (size_t)start; }
 };
 
@@ -533,7 +545,7 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __
     Key key = 0;
     if (i < n) {
         key = keys[i];
-        isStart = key != dead && (i == 0 || keys[i - 1] != key);
+        isStart = key != dead && tgt.live(key) && (i == 0 || keys[i - 1] != key);
         // sorted: a run starting at i has >= kLongRun records iff position i + kLongRun - 1 has its key
         isLong = isStart && i + kLongRun - 1 < n && keys[i + kLongRun - 1] == key;
     }
@@ -541,7 +553,7 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __
         float* e = tgt.at(key, i);
         float acc[9];
         for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * S + c];
+            for (int c = 0; c < 3; ++c) acc[r * 3 + c] = Tgt::kFromZero ? 0.f : e[r * S + c];
         for (int j0 = i; j0 < i + kLongRun; j0 += kFoldBatch) {
             bool in[kFoldBatch];
             float m[kFoldBatch][9];
@@ -569,7 +581,7 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __
         const int start = blockIdx.x * 64 + __ffsll((long long)starts) - 1;
         const Key lkey = keys[start];
         float* e = tgt.at(lkey, start);
-        float acc = lane < 9 ? e[r * S + c] : 0.f;
+        float acc = lane < 9 && !Tgt::kFromZero ? e[r * S + c] : 0.f;
         for (int j0 = start;; j0 += 64) {
             const int j = j0 + lane;
             const bool in = j < n && keys[j] == lkey;
@@ -898,33 +910,32 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         k_fold_runs<NodeRow, true, unsigned><<<cdiv(nA, 64), 64, 0, s>>>(
             nA, 0xffffffffu, P<unsigned>(h->caKeysS), P<int>(h->caIdsS), P<float>(h->caVal),
             NodeRow{P<float>(h->additional)});
+    fc = FineContacts{P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
+                      RecKey::kLaneBits};
+    if (h->factorVariant >= 4) {
+        if (nD > 0) {
+            // each level-0 entry's contact run folded from zero once (the fused
+            // kernel adds it to its zero entry)
+            if ((rc = ensure(h, h->cFineVal, (size_t)nD * 36))) return rc;
+            k_fold_runs<RunSlot, true, unsigned long long><<<cdiv(nD, 64), 64, 0, s>>>(
+                nD, ~0ull, P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal),
+                RunSlot{P<float>(h->cFineVal), (unsigned)begin1});
+            fa.ckeys = P<unsigned long long>(h->cdKeysS);
+            fa.cval = P<float>(h->cFineVal);
+            fa.coff = P<int>(h->cFineOff);
+            fa.B = RecKey::kLaneBits;
+        }
+        // the level-0 blocks need nothing below (pushes and coarse entries):
+        // they start now, before the push count's host round trip
+        if ((rc = fork_fused(h, fa, s))) return rc;
+        forked = true;
+    }
     k_push_count<<<cdiv(nA + 1, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), gn, P<int>(h->cpCnt));
     if ((rc = exclusive_scan(h, P<int>(h->cpCnt), P<int>(h->cpOff), nA + 1, s, "push scan"))) return rc;
     int nP = 0;
     if ((rc = hip_check(h, hipMemcpyAsync(&nP, P<int>(h->cpOff) + nA, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
         (rc = hip_check(h, hipStreamSynchronize(s), "push count sync")))
         return rc;
-    fc = FineContacts{P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
-                      RecKey::kLaneBits};
-    if (h->factorVariant >= 4) {
-        if (fineEnd > 0) {
-            // each level-0 entry's contact run folded from zero once, stored at
-            // the run's first position (the fused kernel adds it to its zero entry)
-            if ((rc = ensure(h, h->cFineVal, (size_t)fineEnd * 36)) ||
-                (rc = hip_check(h, hipMemsetAsync(h->cFineVal.p, 0, (size_t)fineEnd * 36, s), "memset fine contacts")))
-                return rc;
-            k_fold_runs<RunSlot, true, unsigned long long><<<cdiv(fineEnd, 64), 64, 0, s>>>(
-                fineEnd, ~0ull, P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal),
-                RunSlot{P<float>(h->cFineVal)});
-            fa.ckeys = P<unsigned long long>(h->cdKeysS);
-            fa.cval = P<float>(h->cFineVal);
-            fa.coff = P<int>(h->cFineOff);
-            fa.B = RecKey::kLaneBits;
-        }
-        // the level-0 blocks need nothing below: they start now
-        if ((rc = fork_fused(h, fa, s))) return rc;
-        forked = true;
-    }
     const RecKey rk{0, B};
     if (nD > fineEnd)
         k_fold_runs<DenseEntry, true, unsigned long long><<<cdiv(nD - fineEnd, 64), 64, 0, s>>>(
