@@ -71,9 +71,6 @@ __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int no
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic only: when the list has landed
     MAS_STAMP(1, pw, 5);
 #endif
-    // in case this node arrives last: the block's inverse, issued after the
-    // list loads so the first barrier does not wait for it
-    if (w == 1) load_record<true>(inv, blk, lane, g, tl);
     float acc = 0.f;
     if (w == 0) __builtin_amdgcn_s_setprio(3);  // the fold is the launch's longest chain
     for (int b0 = 0; b0 < len; b0 += kDeepChunk) {
@@ -87,6 +84,10 @@ __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int no
         }
         __syncthreads();
         if (b0 == 0) MAS_STAMP(1, pw, 1);
+        // in case this node arrives last: the block's inverse, issued once the
+        // list is staged and in flight during the fold (issued with the list
+        // loads, the staging waits held the barrier: pre-fine 19.3 -> 18.4 us)
+        if (b0 == 0 && w == 1) load_record<true>(inv, blk, lane, g, tl);
         if (b0 + kDeepChunk < len) load(b0 + kDeepChunk);  // in flight during the fold
         if (t < 3) {
             // cnt is a multiple of 32 (stride): whole 8-float4 batches, the
