@@ -46,6 +46,9 @@ namespace mas {
 
 static int bit_width(unsigned x) { return x ? 32 - __builtin_clz(x) : 0; }
 
+// block-entry sort keys (RecKey below): 32 bits, enough for 2^27 nodes
+using EntryKey = unsigned;
+
 struct EdgeRec {
     int lam;  // first common-bank level, 1..L-1
     int row;  // anc_lam(u) (global node id)
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restr
 __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restrict__ st, int n,
                                                        const int* __restrict__ gn, int L,
                                                        const int* __restrict__ dOff, const int* __restrict__ aOff,
-                                                       unsigned long long* __restrict__ dKeys, int* __restrict__ dIds,
+                                                       EntryKey* __restrict__ dKeys, int* __restrict__ dIds,
                                                        float* __restrict__ dVal, unsigned* __restrict__ aKeys,
                                                        int* __restrict__ aIds, float* __restrict__ aVal) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -162,8 +165,8 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
             float t[9];
             for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e]);
             // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot]
-            dKeys[d] = ((unsigned long long)my << 5) | (ot & 31u);
-            dKeys[d + 1] = ((unsigned long long)ot << 5) | (my & 31u);
+            dKeys[d] = (EntryKey)((my << 5) | (ot & 31u));
+            dKeys[d + 1] = (EntryKey)((ot << 5) | (my & 31u));
             dIds[d] = d;
             dIds[d + 1] = d + 1;
             for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
 // Per level-0 block, the range of its contact block-entry records in the
 // sorted array (rows < begin_1 sort first): fineOff[b] .. fineOff[b + 1].
 __global__ __launch_bounds__(256) void k_contact_fine_bounds(int nD, int B, int begin1, int nFineBlk,
-                                                             const unsigned long long* __restrict__ keys,
+                                                             const EntryKey* __restrict__ keys,
                                                              int* __restrict__ fineOff) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > nD) return;
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(256) void k_push_write(int nA, int begin1, int tc, 
 // component e of every entry -- the reference adds PrepareCollisionHessian's
 // terms before PrepareHessian's (.cpp:88-97).
 struct FineContacts {
-    const unsigned long long* keys;  // sorted block-entry keys row * 32 + (col & 31) (RecKey)
+    const EntryKey* keys;  // sorted block-entry keys row * 32 + (col & 31) (RecKey)
     const int* ids;                  // record index -> 9 column-major floats in val
     const float* val;
     const int* off;                  // per level-0 block: first record (nFineBlk + 1)
@@ -285,7 +288,7 @@ __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* _
         const int r = lane / 3, c = lane % 3;
         const int j1 = fc.off[blk + 1];
         for (int j = fc.off[blk]; j < j1; ++j) {
-            const unsigned long long k = fc.keys[j];
+            const EntryKey k = fc.keys[j];
             const unsigned row = (unsigned)(k >> fc.B), col = (unsigned)(k & ((1ull << fc.B) - 1));
             float* e = tile + (3 * (row & 31) + r) * 96 + 3 * (col & 31) + c;
             *e = __fadd_rn(*e, fc.val[9 * (size_t)fc.ids[j] + c * 3 + r]);
@@ -391,18 +394,17 @@ __global__ __launch_bounds__(256) void k_od(FineAsm a, float* __restrict__ od, i
 // relative to begin1 and the column's lane: key = (row - begin1) * 32 +
 // (col & 31), B + 5 bits (B = bit width of the node count above begin1: 16 at
 // 1M, 18 at 4M) instead of 2B -- the stable radix sort runs 3 passes instead
-// of 4 (1M) and 5 (4M).  A dead record's key has all B + 5 bits set, above
-// every live key.  Contact block entries use the same form with begin1 = 0.
+// of 4 (1M) and 5 (4M), over 32-bit keys (half the bytes per pass of the
+// 64-bit ones).  A dead record's key has all B + 5 bits set, above every live
+// key.  Contact block entries use the same form with begin1 = 0.
 struct RecKey {
     int begin1, B;
     static constexpr int kLaneBits = 5;
     __host__ __device__ int bits() const { return B + kLaneBits; }
-    __host__ __device__ unsigned long long dead() const { return (1ull << bits()) - 1; }
-    __device__ unsigned long long pack(unsigned row, unsigned col) const {
-        return ((unsigned long long)(row - begin1) << kLaneBits) | (col & 31u);
-    }
-    __device__ unsigned row(unsigned long long k) const { return (unsigned)(k >> kLaneBits) + begin1; }
-    __device__ unsigned col(unsigned long long k) const { return (row(k) & ~31u) | (unsigned)(k & 31u); }
+    __host__ __device__ EntryKey dead() const { return bits() >= 32 ? ~0u : (1u << bits()) - 1; }
+    __device__ EntryKey pack(unsigned row, unsigned col) const { return ((row - begin1) << kLaneBits) | (col & 31u); }
+    __device__ unsigned row(EntryKey k) const { return (k >> kLaneBits) + begin1; }
+    __device__ unsigned col(EntryKey k) const { return (row(k) & ~31u) | (k & 31u); }
 };
 
 // one thread per vertex (neighbour counts <= 8: a 2-D cloth has ~2 cross-bank
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(256) void k_records_vertex(int nV, int L, RecKey rk
                                                  const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                  const int* __restrict__ gn, const int* __restrict__ ranges,
                                                  const int* __restrict__ recOff, EdgeRec* __restrict__ rec,
-                                                 unsigned long long* __restrict__ keys, int* __restrict__ mats) {
+                                                 EntryKey* __restrict__ keys, int* __restrict__ mats) {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nV) return;
     const int o = s2o[v];
@@ -453,7 +455,7 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, RecKey rk, const
                                                  const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                  const int* __restrict__ gn, const int* __restrict__ ranges,
                                                  const int* __restrict__ recOff, EdgeRec* __restrict__ rec,
-                                                 unsigned long long* __restrict__ keys, int* __restrict__ mats) {
+                                                 EntryKey* __restrict__ keys, int* __restrict__ mats) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int v = t / G, k = 1 + t % G;
     const bool has = v < nV && k < nbrNum[v];
@@ -496,8 +498,8 @@ struct DenseEntry {  // block entry (row node, column node) of the dense buffer
     RecKey rk;
     static constexpr int kStride = 96;
     static constexpr bool kFromZero = false;
-    __device__ bool live(unsigned long long) const { return true; }
-    __device__ float* at(unsigned long long k, int) const { return entry(dense, rk.row(k), rk.col(k)); }
+    __device__ bool live(EntryKey) const { return true; }
+    __device__ float* at(EntryKey k, int) const { return entry(dense, rk.row(k), rk.col(k)); }
 };
 struct DenseDiag {  // the diagonal entry of a node
     float* dense;
@@ -521,8 +523,8 @@ struct RunSlot {
     unsigned begin1;
     static constexpr int kStride = 3;
     static constexpr bool kFromZero = true;
-    __device__ bool live(unsigned long long k) const { return (k >> RecKey::kLaneBits) < begin1; }
-    __device__ float* at(unsigned long long, int start) const { return base + 9 * (size_t)start; }
+    __device__ bool live(EntryKey k) const { return (k >> RecKey::kLaneBits) < begin1; }
+    __device__ float* at(EntryKey, int start) const { return base + 9 * (size_t)start; }
 };
 
 // One wave per 64 sorted positions: the lanes find the runs starting there;
@@ -866,6 +868,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     const int* gn = P<int>(h->goingNext);
     const DevStencil* st = P<DevStencil>(h->stencils);
     int rc;
+    if (B + RecKey::kLaneBits > 32) return fail(h, MAS_ERR_ARG, "contact entry keys: more than 2^27 nodes");
     if ((rc = ensure(h, h->cdCnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->cdOff, (size_t)(n + 1) * 4)) ||
         (rc = ensure(h, h->caCnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->caOff, (size_t)(n + 1) * 4)) ||
         (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4)))
@@ -881,7 +884,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         return rc;
     const int nD = tot[0], nA = tot[1];
     const size_t d1 = nD > 0 ? nD : 1, a1 = nA > 0 ? nA : 1;
-    if ((rc = ensure(h, h->cdKeys, d1 * 8)) || (rc = ensure(h, h->cdKeysS, d1 * 8)) ||
+    if ((rc = ensure(h, h->cdKeys, d1 * 4)) || (rc = ensure(h, h->cdKeysS, d1 * 4)) ||
         (rc = ensure(h, h->cdIds, d1 * 4)) || (rc = ensure(h, h->cdIdsS, d1 * 4)) ||
         (rc = ensure(h, h->cdVal, d1 * 36)) || (rc = ensure(h, h->caKeys, a1 * 4)) ||
         (rc = ensure(h, h->caKeysS, a1 * 4)) || (rc = ensure(h, h->caIds, a1 * 4)) ||
@@ -889,10 +892,10 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         (rc = ensure(h, h->cpCnt, (a1 + 1) * 4)) || (rc = ensure(h, h->cpOff, (a1 + 1) * 4)))
         return rc;
     k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdOff), P<int>(h->caOff),
-                                                 P<unsigned long long>(h->cdKeys), P<int>(h->cdIds),
+                                                 P<EntryKey>(h->cdKeys), P<int>(h->cdIds),
                                                  P<float>(h->cdVal), P<unsigned>(h->caKeys), P<int>(h->caIds),
                                                  P<float>(h->caVal));
-    if ((rc = sort_pairs(h, P<unsigned long long>(h->cdKeys), P<unsigned long long>(h->cdKeysS), P<int>(h->cdIds),
+    if ((rc = sort_pairs(h, P<EntryKey>(h->cdKeys), P<EntryKey>(h->cdKeysS), P<int>(h->cdIds),
                          P<int>(h->cdIdsS), nD, B + RecKey::kLaneBits, s, "contact entry sort")) ||
         (rc = sort_pairs(h, P<unsigned>(h->caKeys), P<unsigned>(h->caKeysS), P<int>(h->caIds), P<int>(h->caIdsS), nA,
                          B, s, "contact row sort")))
@@ -900,7 +903,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     float* dense = dense_base(h);
     // fine entries: k_level0_block; coarse entries: folded onto the zeroed coarse blocks
     k_contact_fine_bounds<<<cdiv(nD + 1, 256), 256, 0, s>>>(nD, RecKey::kLaneBits, begin1, h->nFineBlk,
-                                                            P<unsigned long long>(h->cdKeysS), P<int>(h->cFineOff));
+                                                            P<EntryKey>(h->cdKeysS), P<int>(h->cFineOff));
     int fineEnd = 0;
     if ((rc = hip_check(h, hipMemcpyAsync(&fineEnd, P<int>(h->cFineOff) + h->nFineBlk, 4, hipMemcpyDeviceToHost, s),
                         "D2H")))
@@ -910,17 +913,17 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         k_fold_runs<NodeRow, true, unsigned><<<cdiv(nA, 64), 64, 0, s>>>(
             nA, 0xffffffffu, P<unsigned>(h->caKeysS), P<int>(h->caIdsS), P<float>(h->caVal),
             NodeRow{P<float>(h->additional)});
-    fc = FineContacts{P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
+    fc = FineContacts{P<EntryKey>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
                       RecKey::kLaneBits};
     if (h->factorVariant >= 4) {
         if (nD > 0) {
             // each level-0 entry's contact run folded from zero once (the fused
             // kernel adds it to its zero entry)
             if ((rc = ensure(h, h->cFineVal, (size_t)nD * 36))) return rc;
-            k_fold_runs<RunSlot, true, unsigned long long><<<cdiv(nD, 64), 64, 0, s>>>(
-                nD, ~0ull, P<unsigned long long>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal),
+            k_fold_runs<RunSlot, true, EntryKey><<<cdiv(nD, 64), 64, 0, s>>>(
+                nD, ~0u, P<EntryKey>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal),
                 RunSlot{P<float>(h->cFineVal), (unsigned)begin1});
-            fa.ckeys = P<unsigned long long>(h->cdKeysS);
+            fa.ckeys = P<EntryKey>(h->cdKeysS);
             fa.cval = P<float>(h->cFineVal);
             fa.coff = P<int>(h->cFineOff);
             fa.B = RecKey::kLaneBits;
@@ -938,8 +941,8 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         return rc;
     const RecKey rk{0, B};
     if (nD > fineEnd)
-        k_fold_runs<DenseEntry, true, unsigned long long><<<cdiv(nD - fineEnd, 64), 64, 0, s>>>(
-            nD - fineEnd, ~0ull, P<unsigned long long>(h->cdKeysS) + fineEnd, P<int>(h->cdIdsS) + fineEnd,
+        k_fold_runs<DenseEntry, true, EntryKey><<<cdiv(nD - fineEnd, 64), 64, 0, s>>>(
+            nD - fineEnd, ~0u, P<EntryKey>(h->cdKeysS) + fineEnd, P<int>(h->cdIdsS) + fineEnd,
             P<float>(h->cdVal), DenseEntry{dense, rk});
     if (nP > 0) {
         if ((rc = ensure(h, h->cpKeys, (size_t)nP * 4)) || (rc = ensure(h, h->cpKeysS, (size_t)nP * 4)) ||
@@ -1012,12 +1015,13 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         (rc = hip_check(h, hipStreamSynchronize(s), "nRec sync")))
         return rc;
     const size_t nr = nRec > 0 ? nRec : 1;
-    if ((rc = ensure(h, h->rec, nr * sizeof(EdgeRec))) || (rc = ensure(h, h->recKeys, nr * 8)) ||
-        (rc = ensure(h, h->recKeysSorted, nr * 8)) || (rc = ensure(h, h->recIds, nr * 4)) ||
+    if ((rc = ensure(h, h->rec, nr * sizeof(EdgeRec))) || (rc = ensure(h, h->recKeys, nr * 4)) ||
+        (rc = ensure(h, h->recKeysSorted, nr * 4)) || (rc = ensure(h, h->recIds, nr * 4)) ||
         (rc = ensure(h, h->recIdsSorted, nr * 4)))
         return rc;
     EdgeRec* rec = P<EdgeRec>(h->rec);
     const RecKey rk{h->levelSize[3], bit_width((unsigned)(tc - h->levelSize[3]))};
+    if (rk.bits() > 32) return fail(h, MAS_ERR_ARG, "record keys: more than 2^27 coarse nodes");
     // lanes per vertex: the largest neighbour count (slot 0 is the vertex), rounded to a power of two
     const int valence = h->maxNbr - 1;
     const int lanesPerVertex = valence <= 8 ? 8 : valence <= 16 ? 16 : valence <= 32 ? 32 : 64;
@@ -1026,24 +1030,24 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         constexpr int G = decltype(gtag)::value;
         k_records<G><<<cdiv(nV * G, 256), 256, 0, s>>>(nV, L, rk, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr),
                                                        gn, d_ranges, P<int>(h->recOff), rec,
-                                                       P<unsigned long long>(h->recKeys), P<int>(h->recIds));
+                                                       P<EntryKey>(h->recKeys), P<int>(h->recIds));
     };
     switch (lanesPerVertex) {
         case 8:
             k_records_vertex<<<cdiv(nV, 256), 256, 0, s>>>(nV, L, rk, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr),
                                                            gn, d_ranges, P<int>(h->recOff), rec,
-                                                           P<unsigned long long>(h->recKeys), P<int>(h->recIds));
+                                                           P<EntryKey>(h->recKeys), P<int>(h->recIds));
             break;
         case 16: recordLaunch(std::integral_constant<int, 16>{}); break;
         case 32: recordLaunch(std::integral_constant<int, 32>{}); break;
         default: recordLaunch(std::integral_constant<int, 64>{}); break;
     }
     if (nRec > 0) {
-        if ((rc = sort_pairs(h, P<unsigned long long>(h->recKeys), P<unsigned long long>(h->recKeysSorted),
+        if ((rc = sort_pairs(h, P<EntryKey>(h->recKeys), P<EntryKey>(h->recKeysSorted),
                              P<int>(h->recIds), P<int>(h->recIdsSorted), nRec, rk.bits(), s, "record sort")))
             return rc;
-        k_fold_runs<DenseEntry, true, unsigned long long><<<cdiv(nRec, 64), 64, 0, s>>>(
-            nRec, rk.dead(), P<unsigned long long>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
+        k_fold_runs<DenseEntry, true, EntryKey><<<cdiv(nRec, 64), 64, 0, s>>>(
+            nRec, rk.dead(), P<EntryKey>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
             DenseEntry{dense, rk});
     }
     k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);

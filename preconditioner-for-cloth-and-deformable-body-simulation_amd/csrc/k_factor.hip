@@ -457,9 +457,9 @@ __device__ __forceinline__ void build_slab(const FineAsm& a, int blk, float* S, 
     __syncthreads();
     if (a.ckeys) {  // contact entries of rows in this slab: distinct keys -> distinct entries
         const int j1 = a.coff[blk + 1];
-        const unsigned long long colMask = (1ull << a.B) - 1;
+        const unsigned colMask = (1u << a.B) - 1;
         for (int j = a.coff[blk] + lane; j < j1; j += 64) {
-            const unsigned long long key = a.ckeys[j];
+            const unsigned key = a.ckeys[j];
             const bool start = j == 0 || a.ckeys[j - 1] != key;
             const int nl = (int)((key >> a.B) & 31) - 16 * H, col = (int)(key & colMask) & 31;
             if (start && nl >= 0 && nl < 16) {

@@ -64,7 +64,7 @@ struct FineAsm {
     const float* off9;
     const int* ranges;
     const float* additional;
-    const unsigned long long* ckeys;  // sorted block-entry keys row * 32 + (col & 31) (null: no contacts)
+    const unsigned* ckeys;            // sorted block-entry keys row * 32 + (col & 31) (null: no contacts)
     const float* cval;                // row-major 3x3 per run start
     const int* coff;                  // per level-0 block: first record (nFineBlk + 1)
     int B;
