@@ -37,7 +37,7 @@ constexpr int kDeepChunk = 2048;  // list entries staged per step (8 per thread)
 // last arriving node solves the block.  The whole workgroup (kApplyThreads)
 // runs it.  List p of node T: T * stride + i.  INDEXED (the per-level form and
 // the sharded apply): d.src[d.idx[p]] (-1: padding); else d.src[p] (deepR1).
-template <bool INDEXED>
+template <bool INDEXED, bool PREFETCH = true>
 __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int node, const DeepArgs& d,
                                           float4* __restrict__ rc, float4* __restrict__ zc, int begin1) {
     __shared__ __attribute__((aligned(16))) float st[3][kDeepChunk];  // b128 reads: 16-byte aligned rows
@@ -87,7 +87,7 @@ __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int no
         // in case this node arrives last: the block's inverse, issued once the
         // list is staged and in flight during the fold (issued with the list
         // loads, the staging waits held the barrier: pre-fine 19.3 -> 18.4 us)
-        if (b0 == 0 && w == 1) load_record<true>(inv, blk, lane, g, tl);
+        if (PREFETCH && b0 == 0 && w == 1) load_record<true>(inv, blk, lane, g, tl);
         if (b0 + kDeepChunk < len) load(b0 + kDeepChunk);  // in flight during the fold
         if (t < 3) {
             // cnt is a multiple of 32 (stride): whole 8-float4 batches, the
@@ -134,6 +134,7 @@ __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int no
     MAS_STAMP(1, pw, 3);
     if (!last || w != 1) return;
     if (lane == 0) d.cnt[blk - d.lv3Begin / 32] = 0;  // for the next apply (visible after this kernel)
+    if (!PREFETCH) load_record<true>(inv, blk, lane, g, tl);
     const int n = lane & 31;
     const float4 R = ld_wt(rc + blk * 32 + n - begin1);
     const float3 out = block_solve(g, tl, make_float3(R.x, R.y, R.z), lane);

@@ -95,6 +95,29 @@ __device__ __forceinline__ float3 fold32(const float4* __restrict__ row, unsigne
     return make_float3(ax, ay, az);
 }
 
+// the same fold over 32 children stored component-major (three float rows)
+__device__ __forceinline__ float3 fold32_soa(const float* __restrict__ rx, const float* __restrict__ ry,
+                                             const float* __restrict__ rz) {
+    float ax = 0.f, ay = 0.f, az = 0.f;
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 8) {
+        float vx[8], vy[8], vz[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            vx[k] = rx[k0 + k];
+            vy[k] = ry[k0 + k];
+            vz[k] = rz[k0 + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            ax = __fadd_rn(ax, vx[k]);
+            ay = __fadd_rn(ay, vy[k]);
+            az = __fadd_rn(az, vz[k]);
+        }
+    }
+    return make_float3(ax, ay, az);
+}
+
 // R1 of level-1 bank `bank` (nodes c0 .. c0 + 31, c0 = 32 bank).  l1src holds
 // 32 original vertex ids per node (-1 where the lane is not a child), so the
 // bank's 1 024 slots are one contiguous 4 KiB run: lane L loads slots
@@ -108,6 +131,10 @@ __device__ __forceinline__ float3 fold32(const float4* __restrict__ row, unsigne
 // load took 1.8 us).
 constexpr int kRestrictWaves = 2;  // waves (level-1 banks) per workgroup
 
+// SOA: the children's values staged component-major (12.7 KB of LDS per wave
+// instead of 16.9): 3 waves per SIMD instead of 2 (LDS-bound), which matters
+// when the launch has several rounds of waves (4M tet: 6 530 banks).
+template <bool SOA>
 __global__ __launch_bounds__(64 * kRestrictWaves) void k_restrict12(int n1, int begin1, int L,
                                                                     const int* __restrict__ l1src,
                                                                     const int* __restrict__ goingNext,
@@ -118,7 +145,10 @@ __global__ __launch_bounds__(64 * kRestrictWaves) void k_restrict12(int n1, int 
                                                                     float4* __restrict__ deepR1,
                                                                     const int* __restrict__ done) {
     if (done && *done) return;
-    __shared__ float4 sv[kRestrictWaves][32][33];  // [node][child], padded row
+    constexpr int kRows = SOA ? 1 : kRestrictWaves;
+    constexpr int kCols = SOA ? 1 : 33;
+    __shared__ float4 sv[kRows][32][kCols];  // [node][child], padded row (!SOA)
+    __shared__ float svs[SOA ? kRestrictWaves : 1][3][32][33];  // SOA: [component][node][child]
     __shared__ float4 red[kRestrictWaves][32];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 31;
     const int c0 = (blockIdx.x * kRestrictWaves + w) * 32;
@@ -137,12 +167,22 @@ __global__ __launch_bounds__(64 * kRestrictWaves) void k_restrict12(int n1, int 
 #pragma unroll
     for (int q = 0; q < 16; ++q) val[q] = src[q] >= 0 ? r[src[q]] : make_float4(0.f, 0.f, 0.f, 0.f);
     const unsigned pmsk = own && L >= 3 ? (unsigned)members[parent].y : 0u;  // the parent's children
+    if (SOA) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) sv[w][2 * q + (lane >> 5)][j] = val[q];
+        for (int q = 0; q < 16; ++q) {
+            svs[w][0][2 * q + (lane >> 5)][j] = val[q].x;
+            svs[w][1][2 * q + (lane >> 5)][j] = val[q].y;
+            svs[w][2][2 * q + (lane >> 5)][j] = val[q].z;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sv[w][2 * q + (lane >> 5)][j] = val[q];
+    }
     MAS_STAMP(0, c0 / 32, 1);
     __builtin_amdgcn_wave_barrier();
     // R1: the node's children in lane order from +0 (non-children are +0.0)
-    const float3 a = own ? fold32<false>(sv[w][j], 0u) : make_float3(0.f, 0.f, 0.f);
+    float3 a = make_float3(0.f, 0.f, 0.f);
+    if (own) a = SOA ? fold32_soa(svs[w][0][j], svs[w][1][j], svs[w][2][j]) : fold32<false>(sv[w][j], 0u);
     if (lane < 32) red[w][j] = make_float4(a.x, a.y, a.z, 0.f);  // lanes j and 32 + j share the slot
     __builtin_amdgcn_wave_barrier();
     // R2 of the level-2 nodes whose children are this bank's components (lowest lane)
@@ -168,12 +208,16 @@ struct Solve12 {
 // Workgroups [0, nDeepNodes): one level-3 node each (R1 from deepR1).  The
 // rest: one wave per block of levels 1 and 2, Z = Inv R with R from
 // k_restrict12.
+// PREFETCH (deep_node): the level-3 block's inverse in flight during the fold
+// (182 VGPRs, 2 waves per SIMD); without it more waves per SIMD for the
+// level-1 and level-2 solves, which matters once they take several rounds.
+template <bool PREFETCH>
 __global__ __launch_bounds__(kApplyThreads) void k_solve123(const float4* __restrict__ inv, DeepArgs d,
                                                            float4* __restrict__ rc, float4* __restrict__ zc,
                                                            Solve12 q, const int* __restrict__ done) {
     if (done && *done) return;
     if ((int)blockIdx.x < q.nDeepNodes) {  // workgroup-uniform
-        deep_node<false>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, q.begin1);
+        deep_node<false, PREFETCH>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, q.begin1);
         return;
     }
     // The level-1/2 solves have slack (~4 us of work beside the ~11 us
@@ -247,9 +291,18 @@ void launch_coarse_deep(mas_context* h, const float4* src, const int* idx, hipSt
 void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
     const int begin1 = h->levelSize[3];
     const int n1 = h->levelSize[2];
-    k_restrict12<<<cdiv(ceil32(n1) / 32, kRestrictWaves), 64 * kRestrictWaves, 0, s>>>(
-        n1, begin1, h->L, P<int>(h->l1src), P<int>(h->goingNext), P<int2>(h->members), r, P<float4>(h->Rc),
-        P<int>(h->deepPos), P<float4>(h->deepR1), h->applyDone);
+    const int nb1 = ceil32(n1) / 32;
+    // the occupancy forms once a launch holds several rounds of waves (A/B: env MAS_COARSE_OCC)
+    const bool occ = h->coarseOcc > 0 || (h->coarseOcc < 0 && nb1 >= kCoarseOccBlocks);
+    const dim3 rg(cdiv(nb1, kRestrictWaves)), rb(64 * kRestrictWaves);
+    if (occ)
+        k_restrict12<true><<<rg, rb, 0, s>>>(n1, begin1, h->L, P<int>(h->l1src), P<int>(h->goingNext),
+                                             P<int2>(h->members), r, P<float4>(h->Rc), P<int>(h->deepPos),
+                                             P<float4>(h->deepR1), h->applyDone);
+    else
+        k_restrict12<false><<<rg, rb, 0, s>>>(n1, begin1, h->L, P<int>(h->l1src), P<int>(h->goingNext),
+                                              P<int2>(h->members), r, P<float4>(h->Rc), P<int>(h->deepPos),
+                                              P<float4>(h->deepR1), h->applyDone);
     Solve12 q{};
     q.begin1 = begin1;
     q.lv1Begin = begin1;
@@ -262,8 +315,13 @@ void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
     q.nb2 = ceil32(q.n2) / 32;
     const DeepArgs d = deep_args(h, P<float4>(h->deepR1), nullptr);
     q.nDeepNodes = deep_nodes(h);
-    k_solve123<<<q.nDeepNodes + cdiv(q.nb1 + q.nb2, kApplyThreads / 64), kApplyThreads, 0, s>>>(
-        P<float4>(h->inv), d, P<float4>(h->Rc), P<float4>(h->Zc), q, h->applyDone);
+    const dim3 sg(q.nDeepNodes + cdiv(q.nb1 + q.nb2, kApplyThreads / 64));
+    if (occ)
+        k_solve123<false><<<sg, kApplyThreads, 0, s>>>(P<float4>(h->inv), d, P<float4>(h->Rc), P<float4>(h->Zc), q,
+                                                       h->applyDone);
+    else
+        k_solve123<true><<<sg, kApplyThreads, 0, s>>>(P<float4>(h->inv), d, P<float4>(h->Rc), P<float4>(h->Zc), q,
+                                                      h->applyDone);
 }
 
 // ---- Prepare: the level-3 descendant lists ----

@@ -29,6 +29,7 @@ constexpr int kBlockF4 = kBlockFloats / 4;  // 1164 float4 per block
 constexpr int kMaxLevels = 5;             // reference B-6
 constexpr int kDenseFloats = 96 * 96;
 constexpr int kProfRing = 4096;          // applies recorded while profiling
+constexpr int kCoarseOccBlocks = 4096;   // level-1 blocks from which the coarse launches use their occupancy forms
 
 // Stencil, SeCollisionElements.h:60-69 (device copy; direction xyz only).
 struct DevStencil {
@@ -118,6 +119,10 @@ struct mas_context {
     // forms and the side-stream overlap were measured slower: DESIGN.md
     // section 4.)
     int coarseMode = 2;
+    // coarse launches in their occupancy forms (k_coarse.hip): -1 = when the
+    // level-1 level has >= kCoarseOccBlocks blocks, 0 = never, 1 = always;
+    // env MAS_COARSE_OCC
+    int coarseOcc = -1;
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     // sharded Prepare (mas_set_prepare_shard): the next Prepare assembles and

@@ -1,5 +1,5 @@
-"""The two-pass coarse launch form (k_coarse_twopass.hip, the default)
-against one launch per coarse level (k_apply.hip).
+"""The two-pass coarse launch form (k_coarse.hip, the default), in both of
+its forms, against one launch per coarse level (k_apply.hip).
 
 Every sum runs in the same order in both forms, so the bar is BITWISE
 equality, per apply, over many back-to-back applies with a different residual
@@ -15,11 +15,14 @@ pytestmark = pytest.mark.gpu
 
 
 def _handles(mesh, L, contacts, monkeypatch):
-    """Per-level (mode 0) and two-pass (2) handles."""
+    """Per-level (mode 0), two-pass (2) and two-pass in its occupancy form
+    (the default from 4 096 level-1 blocks: SoA restriction staging, no
+    level-3 inverse prefetch) handles."""
     import mas_amd
     hs = []
-    for mode in (0, 2):
+    for mode, occ in ((0, 0), (2, 0), (2, 1)):
         monkeypatch.setenv("MAS_COARSE_MODE", str(mode))
+        monkeypatch.setenv("MAS_COARSE_OCC", str(occ))
         hs.append(mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts))
         assert hs[-1].stats()["apply_mode"] == mode
     return hs
@@ -46,11 +49,11 @@ def test_twopass_equals_per_level(kind, W, L, nc, monkeypatch):
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=11) if nc else None
-    P3, P2 = _handles(mesh, L, contacts, monkeypatch)
+    P3, P2, P2o = _handles(mesh, L, contacts, monkeypatch)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 100 + k)).cuda() for k in range(24)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    for PX in (P2,):
+    for PX in (P2, P2o):
         zf = _applies(PX, rs, s)
         for k, (a, b) in enumerate(zip(zf, z3)):
             np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
@@ -68,11 +71,11 @@ def test_twopass_1m_contacts_bitwise_and_oracle(monkeypatch):
     from oracle import Oracle
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    P3, P2 = _handles(mesh, 4, contacts, monkeypatch)
+    P3, P2, P2o = _handles(mesh, 4, contacts, monkeypatch)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 0x5EED + k)).cuda() for k in range(40)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    for PX in (P2,):
+    for PX in (P2, P2o):
         zf = _applies(PX, rs, s)
         for k, (a, b) in enumerate(zip(zf, z3)):
             np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
