@@ -53,7 +53,10 @@
 
 namespace mas {
 
-constexpr int kPcgThreads = 256;
+#ifndef MAS_PCG_THREADS
+#define MAS_PCG_THREADS 512
+#endif
+constexpr int kPcgThreads = MAS_PCG_THREADS;
 constexpr int kPcgBlocks = 1024;  // fixed grid: partial sums in a fixed order
 
 struct PcgState {
