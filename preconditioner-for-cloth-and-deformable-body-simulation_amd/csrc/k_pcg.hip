@@ -57,6 +57,9 @@ namespace mas {
 #define MAS_PCG_THREADS 512
 #endif
 constexpr int kPcgThreads = MAS_PCG_THREADS;
+#ifndef MAS_SPMV_NT
+#define MAS_SPMV_NT 1
+#endif
 constexpr int kPcgBlocks = 1024;  // fixed grid: partial sums in a fixed order
 
 struct PcgState {
@@ -179,9 +182,18 @@ __device__ __forceinline__ void spmv_rows_ell(int base, int nV, int lane, const 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         v[r] = base + r * (64 / G) + lane / G;
-        nb[r] = ellIdx[(size_t)(g0 + r) * 64 + lane];
+        // the matrix streams once per SpMV (302 MB at 1M, beyond the Infinity
+        // Cache): nontemporal, so it does not evict the gathered vector
+        if (MAS_SPMV_NT) {
+            nb[r] = __builtin_nontemporal_load(ellIdx + (size_t)(g0 + r) * 64 + lane);
 #pragma unroll
-        for (int q = 0; q < 9; ++q) m[r][q] = ellOff[(size_t)(g0 + r) * 576 + q * 64 + lane];
+            for (int q = 0; q < 9; ++q)
+                m[r][q] = __builtin_nontemporal_load(ellOff + (size_t)(g0 + r) * 576 + q * 64 + lane);
+        } else {
+            nb[r] = ellIdx[(size_t)(g0 + r) * 64 + lane];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) m[r][q] = ellOff[(size_t)(g0 + r) * 576 + q * 64 + lane];
+        }
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {  // only rows longer than G read the CSR arrays
