@@ -267,8 +267,22 @@ __device__ __forceinline__ void block_partial(double a, double* __restrict__ par
 __device__ __forceinline__ double sum_partials(const double* __restrict__ partial, int n = kPcgBlocks) {
     __shared__ double sa[kPcgThreads];
     __syncthreads();
+    // thread t adds partials t, t + kPcgThreads, ... in order; a batch's loads
+    // are all issued before its first add (the r.z partials of the fine
+    // kernel are 8 456 at 1M: 17 per thread)
+    constexpr int kBatch = 8;
     double t = 0.0;
-    for (int i = threadIdx.x; i < n; i += kPcgThreads) t += partial[i];
+    for (int i0 = threadIdx.x; i0 < n; i0 += kBatch * kPcgThreads) {
+        double v[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int i = i0 + k * kPcgThreads;
+            v[k] = i < n ? partial[i] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)
+            if (i0 + k * kPcgThreads < n) t += v[k];
+    }
     sa[threadIdx.x] = t;
     __syncthreads();
     for (int s = kPcgThreads / 2; s > 0; s >>= 1) {
