@@ -29,8 +29,8 @@
 //                 edge mats and (l = 2) od(u); then the children's tables in
 //                 id order; diag += table.  Terms are flattened in parallel,
 //                 then folded strictly left by one wave per node.
-// Contact stencils (only present in the contact configuration) still
-// accumulate with fp32 atomics, as the reference does at CPU_THREAD_NUM > 1.
+// Contact stencils (only present in the contact configuration) are folded in
+// the reference's single-thread order as well (below, before k_contact_*).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>

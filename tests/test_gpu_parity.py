@@ -262,7 +262,8 @@ def test_4m_tet_parity():
 def test_device_resident_contact_records():
     """contact records and counts handed over in device memory
     (as a GPU collision pass would) give the same preconditioner as host
-    records: same stencils, z equal up to the fp32 contact atomics' order."""
+    records: same stencils, z bitwise equal (the contact assembly is
+    deterministic, in the reference's order)."""
     import torch
     import mas_amd
     from mas_amd import meshgen
