@@ -134,8 +134,8 @@ constexpr int kRestrictWaves = 2;  // waves (level-1 banks) per workgroup
 // SOA: the children's values staged component-major (12.7 KB of LDS per wave
 // instead of 16.9): 3 waves per SIMD instead of 2 (LDS-bound), which matters
 // when the launch has several rounds of waves (4M tet: 6 530 banks).
-template <bool SOA>
-__global__ __launch_bounds__(64 * kRestrictWaves) void k_restrict12(int n1, int begin1, int L,
+template <bool SOA, int WAVES = kRestrictWaves>
+__global__ __launch_bounds__(64 * WAVES) void k_restrict12(int n1, int begin1, int L,
                                                                     const int* __restrict__ l1src,
                                                                     const int* __restrict__ goingNext,
                                                                     const int2* __restrict__ members,
@@ -145,13 +145,13 @@ __global__ __launch_bounds__(64 * kRestrictWaves) void k_restrict12(int n1, int 
                                                                     float4* __restrict__ deepR1,
                                                                     const int* __restrict__ done) {
     if (done && *done) return;
-    constexpr int kRows = SOA ? 1 : kRestrictWaves;
+    constexpr int kRows = SOA ? 1 : WAVES;
     constexpr int kCols = SOA ? 1 : 33;
     __shared__ float4 sv[kRows][32][kCols];  // [node][child], padded row (!SOA)
-    __shared__ float svs[SOA ? kRestrictWaves : 1][3][32][33];  // SOA: [component][node][child]
-    __shared__ float4 red[kRestrictWaves][32];
+    __shared__ float svs[SOA ? WAVES : 1][3][32][33];  // SOA: [component][node][child]
+    __shared__ float4 red[WAVES][32];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane & 31;
-    const int c0 = (blockIdx.x * kRestrictWaves + w) * 32;
+    const int c0 = (blockIdx.x * WAVES + w) * 32;
     MAS_STAMP(0, c0 / 32, 0);
     if (c0 >= n1) return;  // wave-uniform; no workgroup barriers below
     const int* s = l1src + (size_t)c0 * 32;  // l1src covers ceil32(n1) nodes
@@ -205,6 +205,9 @@ struct Solve12 {
     int nDeepNodes;   // level-3 nodes lv3Begin .. + nDeepNodes: the first nDeepNodes workgroups
 };
 
+__device__ __forceinline__ void solve12_wave(const float4* __restrict__ inv, float4* __restrict__ rc,
+                                             float4* __restrict__ zc, const Solve12& q, int w);
+
 // Workgroups [0, nDeepNodes): one level-3 node each (R1 from deepR1).  The
 // rest: one wave per block of levels 1 and 2, Z = Inv R with R from
 // k_restrict12.
@@ -226,11 +229,26 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve123(const float4* __rest
     // fold's SIMDs stay quiet.  pre-fine 21.7 -> 19.4 us at 1M + contacts
     // (sleep 32 / 64 / 127: 19.9 / 19.4 / 19.9 us).
     if (q.nDeepNodes > 0) __builtin_amdgcn_s_sleep(64);
-    const int lane = threadIdx.x & 63, n = lane & 31;
     const int w = (blockIdx.x - q.nDeepNodes) * (kApplyThreads / 64) + (threadIdx.x >> 6);
+    if (w >= q.nb1 + q.nb2) return;  // wave-uniform
+    solve12_wave(inv, rc, zc, q, w);
+}
+
+// L = 3 (no level-3 nodes): one single-wave workgroup per level-1/2 block, so
+// the few hundred block solves spread over every CU instead of a quarter of them
+__global__ __launch_bounds__(64) void k_solve12_narrow(const float4* __restrict__ inv, float4* __restrict__ rc,
+                                                      float4* __restrict__ zc, Solve12 q,
+                                                      const int* __restrict__ done) {
+    if (done && *done) return;
+    solve12_wave(inv, rc, zc, q, blockIdx.x);
+}
+
+// Z = Inv R of level-1/2 block w (levels 1, then 2), one wave
+__device__ __forceinline__ void solve12_wave(const float4* __restrict__ inv, float4* __restrict__ rc,
+                                             float4* __restrict__ zc, const Solve12& q, int w) {
+    const int lane = threadIdx.x & 63, n = lane & 31;
     [[maybe_unused]] const int pw = blockIdx.x * 4 + (threadIdx.x >> 6);
     MAS_STAMP(1, pw, 0);
-    if (w >= q.nb1 + q.nb2) return;  // wave-uniform
     int blk, lvBegin, cnt;
     if (w < q.nb1) {
         blk = q.b1 + w; lvBegin = q.lv1Begin; cnt = q.n1;
@@ -294,8 +312,16 @@ void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
     const int nb1 = ceil32(n1) / 32;
     // the occupancy forms once a launch holds several rounds of waves (A/B: env MAS_COARSE_OCC)
     const bool occ = h->coarseOcc > 0 || (h->coarseOcc < 0 && nb1 >= kCoarseOccBlocks);
+    // single-wave workgroups when there is no level-3 chain (L = 3): the few
+    // hundred coarse waves then spread over every CU (256k: pre-fine 12.7 ->
+    // 11.3 us; at 1M the restriction alone this way measured no gain)
+    const bool narrow = h->coarseNarrow > 0 || (h->coarseNarrow < 0 && h->L == 3);
     const dim3 rg(cdiv(nb1, kRestrictWaves)), rb(64 * kRestrictWaves);
-    if (occ)
+    if (narrow && !occ)
+        k_restrict12<false, 1><<<nb1, 64, 0, s>>>(n1, begin1, h->L, P<int>(h->l1src), P<int>(h->goingNext),
+                                                  P<int2>(h->members), r, P<float4>(h->Rc), P<int>(h->deepPos),
+                                                  P<float4>(h->deepR1), h->applyDone);
+    else if (occ)
         k_restrict12<true><<<rg, rb, 0, s>>>(n1, begin1, h->L, P<int>(h->l1src), P<int>(h->goingNext),
                                              P<int2>(h->members), r, P<float4>(h->Rc), P<int>(h->deepPos),
                                              P<float4>(h->deepR1), h->applyDone);
@@ -316,7 +342,10 @@ void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
     const DeepArgs d = deep_args(h, P<float4>(h->deepR1), nullptr);
     q.nDeepNodes = deep_nodes(h);
     const dim3 sg(q.nDeepNodes + cdiv(q.nb1 + q.nb2, kApplyThreads / 64));
-    if (occ)
+    if (narrow && q.nDeepNodes == 0)
+        k_solve12_narrow<<<q.nb1 + q.nb2, 64, 0, s>>>(P<float4>(h->inv), P<float4>(h->Rc), P<float4>(h->Zc), q,
+                                                     h->applyDone);
+    else if (occ)
         k_solve123<false><<<sg, kApplyThreads, 0, s>>>(P<float4>(h->inv), d, P<float4>(h->Rc), P<float4>(h->Zc), q,
                                                        h->applyDone);
     else

@@ -123,6 +123,7 @@ struct mas_context {
     // level-1 level has >= kCoarseOccBlocks blocks, 0 = never, 1 = always;
     // env MAS_COARSE_OCC
     int coarseOcc = -1;
+    int coarseNarrow = -1;  // single-wave coarse workgroups: -1 = at L = 3, 0 = never, 1 = always (env MAS_COARSE_NARROW)
     int fineVariant = 1;  // 1 = nontemporal inverse loads; env MAS_FINE_VARIANT=0 for A/B (k_apply.hip)
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     // sharded Prepare (mas_set_prepare_shard): the next Prepare assembles and
