@@ -42,13 +42,13 @@ static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThread
 // and emit this workgroup's r.z (fp64; a fixed xor butterfly per wave, then
 // the waves in order) to rzPart[blockIdx.x], so the solver needs no separate
 // pass over r and z.
-template <int NPROL, int VAR, bool RZ>
+template <int NPROL, int VAR, bool RZ, int WPB = kApplyThreads / 64>
 __device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, int blk0, int nFineBlk, int nV,
                                                 const float4* __restrict__ r, const int4* __restrict__ vmap,
                                                 const float4* __restrict__ zc, int begin1, float4* __restrict__ z,
                                                 double* __restrict__ rzPart) {
     const int lane = threadIdx.x & 63, n = lane & 31;
-    const int blk = blk0 + blockIdx.x * (kApplyThreads / 64) + (threadIdx.x >> 6);
+    const int blk = blk0 + blockIdx.x * WPB + (threadIdx.x >> 6);
     const bool bvalid = blk < nFineBlk;
     const int v = blk * 32 + n;
     const bool vvalid = bvalid && v < nV;
@@ -98,6 +98,19 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __re
                                                              double* __restrict__ rzPart) {
     if (RZ && *done) return;
     solve_fine_body<NPROL, VAR, RZ>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, rzPart);
+}
+
+// One wave per workgroup: the default for launches of >= kFineWave1Blocks
+// blocks (MAS_FINE_VARIANT=1; 3 forces it, 4 forces 4-wave workgroups).
+// Measured interleaved on one box: 4M tet 433.5 -> 394.6 us per launch
+// (128 000 blocks), 1M 104.2 -> 107.2 us (32 768 blocks, so kept at 4
+// waves there), 256k unchanged.
+constexpr int kFineWave1Blocks = 65536;
+template <int NPROL>
+__global__ __launch_bounds__(64) void k_solve_fine1(const float4* __restrict__ inv, int blk0, int nFineBlk, int nV,
+                                                   const float4* __restrict__ r, const int4* __restrict__ vmap,
+                                                   const float4* __restrict__ zc, int begin1, float4* __restrict__ z) {
+    solve_fine_body<NPROL, 1, false, 1>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, nullptr);
 }
 
 // Coarse levels, one wave per 32-node block; lane n (half 0) owns node
@@ -247,6 +260,8 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
         else
             k_solve_fine<NPROL, 1, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                        done, rzPart);
+    } else if (var == 3 || (var == 1 && blkEnd - blk0 >= kFineWave1Blocks)) {
+        k_solve_fine1<NPROL><<<blkEnd - blk0, 64, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
     } else if (var == 0) {
         k_solve_fine<NPROL, 0, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                     nullptr, nullptr);
