@@ -100,12 +100,9 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __re
     solve_fine_body<NPROL, VAR, RZ>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, rzPart);
 }
 
-// One wave per workgroup: the default for launches of >= kFineWave1Blocks
-// blocks (MAS_FINE_VARIANT=1; 3 forces it, 4 forces 4-wave workgroups).
-// Measured interleaved on one box: 4M tet 433.5 -> 394.6 us per launch
-// (128 000 blocks), 1M 104.2 -> 107.2 us (32 768 blocks, so kept at 4
-// waves there), 256k unchanged.
-constexpr int kFineWave1Blocks = 65536;
+// A/B (MAS_FINE_VARIANT=3): one wave per workgroup.  Measured interleaved,
+// 4M tet: 433.5 -> 394.6 us per launch on one box, 436.3 -> 472.0 us on
+// another; 1M 104.2 -> 107.2 us; 256k unchanged -- not the default.
 template <int NPROL>
 __global__ __launch_bounds__(64) void k_solve_fine1(const float4* __restrict__ inv, int blk0, int nFineBlk, int nV,
                                                    const float4* __restrict__ r, const int4* __restrict__ vmap,
@@ -260,7 +257,7 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
         else
             k_solve_fine<NPROL, 1, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                        done, rzPart);
-    } else if (var == 3 || (var == 1 && blkEnd - blk0 >= kFineWave1Blocks)) {
+    } else if (var == 3) {
         k_solve_fine1<NPROL><<<blkEnd - blk0, 64, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
     } else if (var == 0) {
         k_solve_fine<NPROL, 0, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,

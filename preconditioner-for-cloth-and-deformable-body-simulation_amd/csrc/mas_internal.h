@@ -125,8 +125,8 @@ struct mas_context {
     int coarseOcc = -1;
     int coarseNarrow = -1;  // single-wave coarse workgroups: -1 = at L = 3, 0 = never, 1 = always (env MAS_COARSE_NARROW)
     // fine kernel (env MAS_FINE_VARIANT, k_apply.hip): 1 = nontemporal inverse
-    // loads, one-wave workgroups from kFineWave1Blocks blocks; 3 / 4 = always
-    // one / four waves per workgroup; 0 = default-policy loads (A/B)
+    // loads (4-wave workgroups); 3 = the same in one-wave workgroups (A/B);
+    // 0 = default-policy loads (A/B)
     int fineVariant = 1;
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     // sharded Prepare (mas_set_prepare_shard): the next Prepare assembles and
