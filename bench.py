@@ -104,30 +104,47 @@ def cpu_info():
 
 
 def cpu_baseline(mesh, cfg, contacts, r_np, steps):
-    # threads pinned close (set before the OpenMP runtime loads)
-    os.environ.setdefault("OMP_PROC_BIND", "close")
+    """OMP_NUM_THREADS = CPU_THREAD_NUM = nproc - 1 (the reference's
+    WIN32 rule, SeOmp.cpp:29-33), threads pinned close.  The box's own
+    OMP_NUM_THREADS (a CPU-share hint) is timed beside it when it differs."""
+    os.environ["OMP_PROC_BIND"] = "close"   # before the OpenMP runtime loads
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from oracle import Oracle  # test infrastructure: the timed CPU baseline only
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or max(1, (os.cpu_count() or 2) - 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 2
+    threads = max(1, ncpu - 1)
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], cfg["levels"], threads)
     o.allocate(mesh)
     if contacts is None:
         o.prepare(mesh)
     else:
         o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
-    for _ in range(3):
-        o.apply(r_np)
-    ts = []
-    for _ in range(steps):
-        t = time.perf_counter()
-        z = o.apply(r_np)
-        ts.append(time.perf_counter() - t)
-    med = statistics.median(ts)
-    return {"value": round(1.0 / med, 3), "unit": "applies/s", "cores": threads, "kind": "port", **cpu_info(),
-            "sample": f"{cfg['name']} workload, oracle/ CPU restatement (OpenMP, {threads} threads, "
-                      f"reference packed layout), median of {steps} applies after 3 warm-up; "
-                      f"ms/apply {med * 1e3:.2f}"}, z
+
+    def timed(n):
+        o.set_threads(n)
+        for _ in range(3):
+            o.apply(r_np)
+        ts = []
+        for _ in range(steps):
+            t = time.perf_counter()
+            z = o.apply(r_np)
+            ts.append(time.perf_counter() - t)
+        return statistics.median(ts), z
+
+    med, z = timed(threads)
+    out = {"value": round(1.0 / med, 3), "unit": "applies/s", "cores": threads, "kind": "port", **cpu_info(),
+           "OMP_NUM_THREADS_env": env_threads or None,
+           "sample": f"{cfg['name']} workload, oracle/ CPU restatement (OpenMP, {threads} threads = nproc - 1, "
+                     f"OMP_PROC_BIND=close, reference packed layout), median of {steps} applies after 3 warm-up; "
+                     f"ms/apply {med * 1e3:.2f}"}
+    if env_threads and env_threads != threads:
+        med2, _ = timed(env_threads)
+        out["at_OMP_NUM_THREADS_env"] = {"threads": env_threads, "value": round(1.0 / med2, 3),
+                                         "ms_per_apply": round(med2 * 1e3, 3)}
+    return out, z
 
 
 PREP_KEYS = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms", "prepare_fine_ms")
@@ -311,7 +328,9 @@ def main():
         L4 = min(info["num_levels"], 4)
         fine_bytes = ((plan["fine_block_end"] - plan["fine_block_begin"]) * BLOCK_BYTES +
                       (plan["vert_end"] - plan["vert_begin"]) * (36 + 4 * (L4 - 1)))
-    traffic = pmc_traffic("k_solve_fine")
+    # the committed PMC figure is one whole-problem launch: a sharded rank's
+    # launch moves only its own slice, so N > 1 lines carry no traffic figure
+    traffic = pmc_traffic("k_solve_fine") if plan is None else (None, None, {})
     fine_s = st["fine_ms_avg"] / 1e3
     achieved = fine_bytes / fine_s / 1e9 if fine_s > 0 else None
     value = args.steps / t_max          # applies of the whole problem per second
@@ -359,9 +378,11 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             "traffic": traffic[0],
-            "traffic_source": f"{traffic[1]}: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                              "passes of this bench command, FETCH_SIZE x2 (gfx950 wide-read correction) + "
-                              "WRITE_SIZE, KB = 1024 B, per launch",
+            "traffic_source": (f"{traffic[1]}: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                               "passes of this bench command, FETCH_SIZE x2 (gfx950 wide-read correction) + "
+                               "WRITE_SIZE, KB = 1024 B, per launch") if traffic[1] else
+                              ("not measured per rank (the committed PMC pass is the whole single-GPU launch)"
+                               if plan is not None else None),
             "traffic_measured_at": traffic[2] or None,
             "bytes_per_launch": fine_bytes,
             "avg_launch_ms": round(st["fine_ms_avg"], 5),
@@ -384,6 +405,9 @@ def main():
                                  "assemble": round(st0["prepare_assemble_ms"], 3),
                                  "factor": round(st0["prepare_factor_ms"], 3),
                                  "level0_fused_overlapped": round(st0["prepare_fine_ms"], 3)},
+        "factor_formation": ("level-0 inverses Inv = L^-T D^-1 L^-1 on the matrix cores (v_mfma_f32_32x32x2_f32)"
+                             if st0.get("factor_formation") == 1 else
+                             "level-0 inverses in the reference's operation order on the vector ALUs"),
         "allocate_ms": round(st0["allocate_ms"], 3),
         "host_setup_s": round(setup_s, 2),
         "wall_s_timed": round(wall, 4),

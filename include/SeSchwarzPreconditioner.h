@@ -98,25 +98,41 @@ static_assert(sizeof(EfSet) == 48 && sizeof(VfSet) == 48 && sizeof(EeSet) == 48,
 static_assert(offsetof(EfSet, m_bary) == 12 && offsetof(VfSet, m_bary) == 16 && offsetof(EfSet, m_normal) == 32,
               "contact record layout");
 
-// SeCsr<int> (SeCsr.h:35-173): rows m_starts[n+1], column ids m_idxs.
+// SeCompressSparseData<Type> / SeCsr<Type> (SeCsr.h:35-173): rows m_starts[n+1],
+// column ids m_idxs.  Same object layout as the reference's class (vtable
+// pointer, then the three vectors; 80 B for SeCsr<int> with libstdc++), pinned
+// against the reference's own header by tests/test_ref_pinned.py.
 template <typename Type>
-class SeCsr {
+class SeCompressSparseData {
   public:
-    SeCsr() {}
-    SeCsr(const std::vector<int>& starts, const std::vector<int>& idxs, const std::vector<Type>& values)
+    SeCompressSparseData() {}
+    SeCompressSparseData(const std::vector<int>& starts, const std::vector<int>& idxs,
+                         const std::vector<Type>& values)
         : m_starts(starts), m_idxs(idxs), m_values(values) {}
-    int Rows() const { return (int)m_starts.size() - 1; }
+    virtual ~SeCompressSparseData() {}
     int Size() const { return m_starts.back(); }
     int Size(int id) const { return m_starts[id + 1] - m_starts[id]; }
     int Start(int id) const { return m_starts[id]; }
     const int* StartPtr(int id) const { return &m_starts[id]; }
+    int Idx(int id) const { return m_idxs[id]; }
     const int* IdxPtr(int id) const { return m_idxs.data() + m_starts[id]; }
     const Type* ValuePtr(int id) const { return m_values.data() + m_starts[id]; }
+    virtual const SeCompressSparseData* Ptr() const { return this; }
 
   protected:
     std::vector<int> m_starts;
     std::vector<int> m_idxs;
     std::vector<Type> m_values;
+};
+
+template <typename Type>
+class SeCsr : public SeCompressSparseData<Type> {
+  public:
+    SeCsr() {}
+    SeCsr(const std::vector<int>& starts, const std::vector<int>& idxs, const std::vector<Type>& values)
+        : SeCompressSparseData<Type>(starts, idxs, values) {}
+    int Rows() const { return (int)SeCompressSparseData<Type>::m_starts.size() - 1; }
+    const SeCsr* Ptr() const override { return this; }
 };
 
 class SeSchwarzPreconditioner {

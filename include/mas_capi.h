@@ -40,7 +40,11 @@
 extern "C" {
 #endif
 
-#define MAS_ABI_VERSION 1
+/* 2: mas_stats / mas_pcg_result grew (prepare_fine_ms, factor_formation,
+ *    first_pass_iterations, replacements) and gained a reserved tail, so later
+ *    additions do not change their size again; mas_config.reference_formation;
+ *    MAS_ERR_COMM. */
+#define MAS_ABI_VERSION 2
 
 typedef enum {
     MAS_OK = 0,
@@ -64,7 +68,12 @@ typedef struct {
     int keep_blocks;   /* 1 = Prepare also stores the assembled level-0 blocks (mas_get_block_matrix on
                           them; +2.4 GB of HBM traffic at 1M).  0 = the fused level-0 assemble + factor
                           never writes them; only the coarse blocks are kept */
-    int reserved[11];
+    int reference_formation; /* 0 = the level-0 inverses Inv = L^-T D^-1 L^-1 are formed on the matrix
+                                cores (default; within 5e-8 of the reference arithmetic, not bitwise);
+                                1 = the reference's own operation order on the vector ALUs
+                                (.cpp:1437-1495): every inverse bitwise equal to the reference
+                                arithmetic, ~0.15 ms more Prepare at 1M */
+    int reserved[10];
 } mas_config;
 
 typedef struct {
@@ -101,6 +110,9 @@ typedef struct {
        factor (default) runs on its own stream beside assemble/factor: prepare_fine_ms
        is its device time (0 when unfused) */
     double prepare_fine_ms;
+    int64_t factor_formation;  /* level-0 inverse formation of the last Prepare: 1 = matrix cores
+                                  (v_mfma_f32_32x32x2_f32), 0 = vector ALUs in the reference's order */
+    int64_t reserved[8];       /* zero; room for later fields without a size change */
 } mas_stats;
 
 /* lifecycle */
@@ -159,6 +171,7 @@ typedef struct {
     int first_pass_iterations; /* iterations until the recursive residual first met tol (0: never) --
                                   what an fp64 PCG would report; the rest drive the fp32 x below tol */
     int replacements;     /* residual replacements (r = b - A x) performed */
+    int reserved[8];      /* zero; room for later fields without a size change */
 } mas_pcg_result;
 int mas_pcg_solve_device(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges,
                          float* d_x4, const float* d_b4, int max_iters, float tol, int precondition,
@@ -279,8 +292,11 @@ int mas_get_neighbors(mas_handle h, int* nbr_num, int* nbr);
 int mas_get_block_matrix(mas_handle h, int blk, float* out96x96);
 int mas_get_block_inverse(mas_handle h, int blk, float* out96x96);
 /* The residual hierarchy of the most recent single-GPU apply
- * (BuildResidualHierarchy .cpp:1548-1598): R of every coarse node, ids
- * begin_1 .. total_clusters-1, as out4[total_clusters - begin_1][4]. */
+ * (BuildResidualHierarchy .cpp:1548-1598) as out4[total_clusters - begin_1][4]
+ * over coarse node ids begin_1 .. total_clusters-1.  Only levels
+ * 1 .. min(L-1, 3) are computed: at L = 5 the level-4 entries are 0 (that
+ * level is never prolonged, CollectFinalZ .cpp:1706-1717, so it is skipped),
+ * where the reference's m_mappedR holds the sums. */
 int mas_get_coarse_residual(mas_handle h, float* out4);
 
 #ifdef __cplusplus

@@ -94,6 +94,11 @@ static inline float se_min(float a, float b) { return a < b ? a : b; } /* SE_MIN
 static inline float se_max(float a, float b) { return a > b ? a : b; } /* SE_MAX, SePreDefine.h:38 */
 /* Math::Clamp = Min(Max(lo, a), hi), SeMath.h:103.  NaN -> hi (B-8). */
 static inline float se_clamp(float a, float lo, float hi) { return se_min(se_max(lo, a), hi); }
+
+/* exported for the reference-pinned tests (tests/test_ref_pinned.py) */
+float orc_clamp(float a, float lo, float hi) { return se_clamp(a, lo, hi); }
+float orc_min(float a, float b) { return se_min(a, b); }
+float orc_max(float a, float b) { return se_max(a, b); }
 static inline int popc32(unsigned v) { return __builtin_popcount(v); }
 static inline int ffs32(unsigned v) { return v ? __builtin_ctz(v) + 1 : 0; } /* Intrinsic::Ffs */
 static inline unsigned lanemask_lt(unsigned lane) { return (1u << lane) - 1u; } /* SeIntrinsic.h:154 */

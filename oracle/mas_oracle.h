@@ -87,6 +87,9 @@ const float* orc_mapped_r(const orc_state* s);    /* m_mappedR [capacity][4] aft
 
 /* The reference's Morton encode of one normalised point (SeMorton.h:75-86). */
 uint64_t orc_morton_encode(float x, float y, float z);
+float orc_clamp(float a, float lo, float hi); /* Math::Clamp, SeMath.h:103 */
+float orc_min(float a, float b);              /* Math::Min, SeMath.h:101 */
+float orc_max(float a, float b);              /* Math::Max, SeMath.h:102 */
 
 #ifdef __cplusplus
 }

@@ -53,6 +53,11 @@ def lib():
         L.orc_block_inverse.argtypes = [_P, _I, _P]
         L.orc_morton_encode.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float]
         L.orc_morton_encode.restype = ctypes.c_uint64
+        L.orc_clamp.argtypes = [ctypes.c_float] * 3
+        L.orc_clamp.restype = ctypes.c_float
+        for name in ("orc_min", "orc_max"):
+            getattr(L, name).argtypes = [ctypes.c_float] * 2
+            getattr(L, name).restype = ctypes.c_float
         _lib = L
     return _lib
 

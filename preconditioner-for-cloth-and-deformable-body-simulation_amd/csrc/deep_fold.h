@@ -15,7 +15,29 @@ namespace mas {
 
 // write-through hand-off of a float4 (agent-scope relaxed atomic stores: sc1,
 // no L2 writeback fence), drained before the arrival counter moves; the
-// consumer reads it with sc1 loads (no invalidate fence)
+// consumer reads it with sc1 loads (no invalidate fence).
+//
+// This is a HARDWARE protocol for gfx942/gfx950, not a C++/HIP memory-model
+// guarantee: in the model, relaxed atomics to different locations give no
+// happens-before edge between producer and consumer.  It rests on these rows
+// of LLVM's AMDGPU memory model for GFX942 (AMDGPUUsage, "Memory Model GFX942",
+// which gfx950 shares):
+//   * store atomic monotonic, agent scope  -> global_store ... sc1: written
+//     through the (per-XCD, non-coherent) L2 to memory-side coherence;
+//   * load atomic monotonic, agent scope   -> global_load ... sc1: misses the
+//     local L2 for that line, reads the coherent copy;
+//   * atomicrmw monotonic, agent scope     -> global_atomic ... sc1, performed
+//     at memory-side coherence.
+// The producer issues its sc1 stores, waits for their completion
+// (s_waitcnt vmcnt(0): the write-through acknowledgements), and only then
+// issues the counter RMW; the consumer issues its sc1 loads only after that
+// RMW has returned the count that makes it the last arriver.  Every datum
+// involved is written and read with sc1, so no L2 copy of it is ever
+// consulted, and the waitcnt orders completion before the count.  The
+// formal alternative -- release fetch_add + acquire fence (buffer_wbl2 sc1 /
+// buffer_inv sc1 on the whole L2) -- measured 4.8 us per hand-off here.
+// Regression test with 18 level-3 blocks spread over every XCD:
+// tests/test_gpu_restrict.py::test_level3_handoff_across_xcds_4m_tet.
 __device__ __forceinline__ void st_wt(float4* p, float4 v) {
     unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
     __hip_atomic_store(q, __builtin_bit_cast(unsigned long long, make_float2(v.x, v.y)), __ATOMIC_RELAXED,

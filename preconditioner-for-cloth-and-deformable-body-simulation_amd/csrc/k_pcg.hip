@@ -48,6 +48,7 @@
 // Every kernel, the apply's included, exits at its first instruction once the
 // solve is done, so the chunks enqueued past convergence cost launches only.
 #include <algorithm>
+#include <cstring>
 
 #include "mas_internal.h"
 
@@ -665,6 +666,7 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
     float ms = 0.f;
     hipEventElapsedTime(&ms, e0, e1);
     if (res) {
+        std::memset(res, 0, sizeof(*res));
         res->iterations = host.iters;
         res->converged = host.rrTrue <= host.tol2 * host.bb;  // the returned x's own residual
         res->rel_residual = host.bb > 0 ? sqrt(host.rr / host.bb) : 0.0;

@@ -356,10 +356,24 @@ int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn a
     if (!h->commStream) {
         if ((rc = hip_check(h, hipStreamCreateWithFlags(&h->commStream, hipStreamNonBlocking), "comm stream")) ||
             (rc = hip_check(h, hipEventCreateWithFlags(&h->evRestrict, hipEventDisableTiming), "event")) ||
-            (rc = hip_check(h, hipEventCreateWithFlags(&h->evGathered, hipEventDisableTiming), "event")))
+            (rc = hip_check(h, hipEventCreateWithFlags(&h->evGathered, hipEventDisableTiming), "event")) ||
+            (rc = hip_check(h, hipEventCreateWithFlags(&h->evShardDone, hipEventDisableTiming), "event")))
             return rc;
     }
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    // The segments (shardSeg, shardGathered, Rc / Zc) belong to the handle: a
+    // call on another stream than the previous one starts after it has ended
+    // (on one stream the order is implicit; the communication stream waits for
+    // this call's restrict, which then follows the previous call's complete).
+    if (h->shardLastStream && h->shardLastStream != s &&
+        (rc = hip_check(h, hipStreamWaitEvent(s, h->evShardDone, 0), "previous apply wait")))
+        return rc;
+    h->shardLastStream = s;
+    struct DoneMark {
+        mas_handle h;
+        hipStream_t s;
+        ~DoneMark() { hipEventRecord(h->evShardDone, s); }
+    } done{h, s};
     float* seg = P<float>(h->shardSeg);
     float* gathered = P<float>(h->shardGathered);
     if ((rc = mas_apply_shard_restrict(h, rank, world, d_r4, seg, s))) return rc;

@@ -92,6 +92,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_OCC")) h->coarseOcc = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_NARROW")) h->coarseNarrow = std::atoi(v);
+    if (h->cfg.reference_formation) h->factorVariant = 4;
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
     int rc = upload_slot_table(h);
@@ -107,6 +108,11 @@ int mas_destroy(mas_handle h) {
     if (!h) return MAS_ERR_ARG;
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
+    // drain every stream this handle enqueued on -- including an allgather of
+    // mas_shard_apply_rccl still writing shardGathered -- before the
+    // communicator and the buffers go
+    if (h->commStream) hipStreamSynchronize(h->commStream);
+    if (h->evShardDone) hipEventSynchronize(h->evShardDone);
     if (h->prepStream) {
         hipStreamSynchronize(h->prepStream);
         hipStreamDestroy(h->prepStream);
@@ -115,17 +121,18 @@ int mas_destroy(mas_handle h) {
     if (h->evPrepJoin) hipEventDestroy(h->evPrepJoin);
     for (auto& e : h->evFine)
         if (e) hipEventDestroy(e);
+    release_comm(h);  // drained above; the communicator goes before the buffers it wrote
     h->for_each_buffer([](Buffer& b) { release(b); });
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
     for (auto& e : h->prof) hipEventDestroy(e);
-    release_comm(h);
     if (h->commStream) {
         hipStreamSynchronize(h->commStream);
         hipStreamDestroy(h->commStream);
     }
     if (h->evRestrict) hipEventDestroy(h->evRestrict);
     if (h->evGathered) hipEventDestroy(h->evGathered);
+    if (h->evShardDone) hipEventDestroy(h->evShardDone);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return MAS_OK;

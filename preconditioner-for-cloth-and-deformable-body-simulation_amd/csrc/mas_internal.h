@@ -112,8 +112,9 @@ struct mas_context {
     // LDS slabs + register-blocked factor, one kernel, overlapped with the
     // coarse assembly on prepStream); 2 = k_level0_block + k_factor_rb;
     // 3 = 2 with the MFMA formation (not bitwise); 5 = 4 with the MFMA
-    // formation (not bitwise); 0 = LDS-row k_factor
-    int factorVariant = 4;
+    // formation (not bitwise, the default; mas_config.reference_formation = 1
+    // selects 4); 0 = LDS-row k_factor
+    int factorVariant = 5;
     // coarse levels (env MAS_COARSE_MODE): 2 = two launches, restrictions then
     // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (One-launch
     // forms and the side-stream overlap were measured slower: DESIGN.md
@@ -180,6 +181,10 @@ struct mas_context {
     mas::Buffer shardSeg, shardGathered;
     hipStream_t commStream = nullptr;
     hipEvent_t evRestrict = nullptr, evGathered = nullptr;
+    // end of the previous mas_shard_apply_device call and the stream it ran
+    // on: a call on another stream waits for it (the segments are the handle's)
+    hipEvent_t evShardDone = nullptr;
+    hipStream_t shardLastStream = nullptr;
     void* rcclComm = nullptr;  // ncclComm_t (comm_rccl.hip)
     int rcclRank = -1, rcclWorld = 0;
     hipEvent_t* shardPendingEv = nullptr;  // profiling events of an overlapped sharded apply in flight

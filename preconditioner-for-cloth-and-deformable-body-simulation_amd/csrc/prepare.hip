@@ -54,6 +54,7 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     float f = 0;
     if (h->factorVariant >= 4 && h->evFine[0]) hipEventElapsedTime(&f, h->evFine[0], h->evFine[1]);
     h->stats.prepare_fine_ms = f;
+    h->stats.factor_formation = (h->factorVariant == 5 || h->factorVariant == 3) ? 1 : 0;
     h->prepared = true;
     return MAS_OK;
 }

@@ -46,7 +46,8 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
 
 class mas_config(ctypes.Structure):
     _fields_ = [("max_levels", ctypes.c_int), ("resort_period", ctypes.c_int), ("fix_vf_bary", ctypes.c_int),
-                ("device", ctypes.c_int), ("keep_blocks", ctypes.c_int), ("reserved", ctypes.c_int * 11)]
+                ("device", ctypes.c_int), ("keep_blocks", ctypes.c_int),
+                ("reference_formation", ctypes.c_int), ("reserved", ctypes.c_int * 10)]
 
 
 class mas_info(ctypes.Structure):
@@ -62,7 +63,8 @@ class mas_stats(ctypes.Structure):
                                                "prepare_assemble_ms", "prepare_factor_ms")] + \
                [("apply_calls", ctypes.c_int64), ("profiled_applies", ctypes.c_int64)] + \
                [(n, ctypes.c_double) for n in ("apply_ms_avg", "pre_fine_ms_avg", "fine_ms_avg", "post_fine_ms_avg")] + \
-               [("apply_mode", ctypes.c_int64), ("prepare_fine_ms", ctypes.c_double)]
+               [("apply_mode", ctypes.c_int64), ("prepare_fine_ms", ctypes.c_double),
+                ("factor_formation", ctypes.c_int64), ("reserved", ctypes.c_int64 * 8)]
 
 
 class mas_shard(ctypes.Structure):
@@ -76,10 +78,11 @@ class mas_shard(ctypes.Structure):
 class mas_pcg_result(ctypes.Structure):
     _fields_ = [("iterations", ctypes.c_int), ("converged", ctypes.c_int), ("rel_residual", ctypes.c_double),
                 ("true_rel_residual", ctypes.c_double), ("solve_ms", ctypes.c_double),
-                ("first_pass_iterations", ctypes.c_int), ("replacements", ctypes.c_int)]
+                ("first_pass_iterations", ctypes.c_int), ("replacements", ctypes.c_int),
+                ("reserved", ctypes.c_int * 8)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
 class MasError(RuntimeError):
@@ -196,9 +199,10 @@ class SeSchwarzPreconditioner:
     """Reference-compatible surface (SE::SeSchwarzPreconditioner) on the GPU."""
 
     def __init__(self, max_levels: int = 0, resort_period: int = 0, fix_vf_bary: bool = False, device: int = -1,
-                 keep_blocks: bool = False):
+                 keep_blocks: bool = False, reference_formation: bool = False):
         self._L = lib()
-        cfg = mas_config(max_levels, resort_period, int(fix_vf_bary), device, int(bool(keep_blocks)))
+        cfg = mas_config(max_levels, resort_period, int(fix_vf_bary), device, int(bool(keep_blocks)),
+                         int(bool(reference_formation)))
         h = ctypes.c_void_p()
         rc = self._L.mas_create(ctypes.byref(h), ctypes.byref(cfg))
         if rc != MAS_OK:
@@ -439,7 +443,7 @@ class SeSchwarzPreconditioner:
     def stats(self) -> dict:
         s = mas_stats()
         self._check(self._L.mas_get_stats(self.h, ctypes.byref(s)), "get_stats")
-        return {k: getattr(s, k) for k, _ in mas_stats._fields_}
+        return {k: getattr(s, k) for k, _ in mas_stats._fields_ if k != "reserved"}
 
     def maps(self) -> dict:
         inf = self.info()

@@ -16,9 +16,9 @@ from conftest import REPO, cloth
 pytestmark = pytest.mark.gpu
 
 
-def _prepared(mesh, L=0, contacts=None):
+def _prepared(mesh, L=0, contacts=None, reference_formation=False):
     import mas_amd
-    return mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
+    return mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, reference_formation=reference_formation)
 
 
 @pytest.mark.parametrize("W,L,nc", [(64, 0, 200), (100, 3, 0)])
@@ -87,7 +87,7 @@ def test_golden_blob_reproduced():
     """Cross-box golden comparison: this box's Allocate + Prepare of the 12x12
     grid gives the committed blob byte for byte (maps, inverses, checksum)."""
     golden = np.fromfile(os.path.join(REPO, "tests", "golden", "cloth12_L0.masblob"), dtype=np.uint8)
-    blob = _prepared(cloth(12)).save_blob()
+    blob = _prepared(cloth(12), reference_formation=True).save_blob()   # inverses in the reference's order
     assert blob.nbytes == golden.nbytes
     np.testing.assert_array_equal(blob, golden)
 

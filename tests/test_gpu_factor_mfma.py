@@ -1,6 +1,7 @@
 """The matrix-core inverse formation (k_factor.hip form_mfma: MAS_FACTOR_VARIANT
-3 = unfused, 5 = inside the fused level-0 kernel) against the reference-order
-VALU formation (the default, bitwise equal to the oracle for equal blocks).
+3 = unfused, 5 = inside the fused level-0 kernel, the library default since
+round 3) against the reference-order VALU formation (mas_config
+.reference_formation = 1, bitwise equal to the oracle for equal blocks).
 
 The elimination is shared, so the two differ only in the order in which the
 96 products of every inverse entry are summed.  Bars: every block's inverse

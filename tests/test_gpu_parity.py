@@ -22,9 +22,24 @@ pytestmark = pytest.mark.gpu
 Z_TOL = 1e-5
 
 
-def _gpu(mesh, L, contacts=None, **kw):
+def _gpu(mesh, L, contacts=None, reference_formation=True, **kw):
+    """A prepared handle.  reference_formation=True (these tests' default):
+    level-0 inverses formed in the reference's operation order, so they are
+    bitwise the oracle's; False: the library default, the matrix-core formation
+    (z within Z_TOL, checked at every BASELINE config below)."""
     import mas_amd
-    return mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, **kw)
+    return mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, reference_formation=reference_formation, **kw)
+
+
+def _z_default_formation(mesh, L, o, seed, contacts=None):
+    """The library default (matrix-core inverse formation) against the oracle."""
+    from mas_amd import meshgen
+    P = _gpu(mesh, L, contacts=contacts, reference_formation=False)
+    assert P.stats()["factor_formation"] == 1
+    r = meshgen.residual(mesh.nV, seed)
+    err = rel_err(P.Preconditioning(None, r), o.apply(r))
+    print(f"nV={mesh.nV} L={L}: default (matrix-core) formation z rel. error {err:.2e}")
+    assert err <= Z_TOL
 
 
 def _oracle(mesh, L, contacts=None, threads=4, fix_vf_bary=False):
@@ -91,6 +106,7 @@ def test_small_configs_parity(kind, W, L):
         z_o = o.apply(r)
         assert rel_err(z_g, z_o) <= Z_TOL, (kind, W, L, rel_err(z_g, z_o))
         assert np.all(z_g[:, 3] == 0.0)
+    _z_default_formation(mesh, L, o, 0x5EED)
 
 
 def test_device_path_and_determinism():
@@ -135,6 +151,7 @@ def test_256k_cloth_parity():
     for seed in (0x5EED + 1, 11):
         r = meshgen.residual(mesh.nV, seed)
         assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
+    _z_default_formation(mesh, cfg["levels"], o, 0x5EED + 1)
 
 
 def test_1m_cloth_parity():
@@ -144,8 +161,10 @@ def test_1m_cloth_parity():
     o = _oracle(mesh, 4, threads=8)
     compare_maps(P, o, mesh.nV)
     assert P.info()["num_blocks"] == 33825
+    assert P.stats()["factor_formation"] == 0
     r = meshgen.residual(mesh.nV, 0x5EED + 3)
     assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
+    _z_default_formation(mesh, 4, o, 0x5EED + 3)
 
 
 def test_1m_contacts_parity():
@@ -177,6 +196,7 @@ def test_1m_contacts_parity():
     with pytest.raises(mas_amd.MasError, match="STATE"):
         Pd.block_matrix(0)
     np.testing.assert_array_equal(Pd.block_matrix(nfine), P.block_matrix(nfine))
+    _z_default_formation(mesh, 4, o, 0x5EED + 2, contacts=contacts)
 
 
 @pytest.mark.parametrize("kind,W,L,nc", [("cloth", 100, 0, 300), ("tet", 16, 3, 0), ("cloth", 33, 0, 0),
@@ -221,7 +241,7 @@ def test_all_contact_types_parity(W, L, n):
     ef, efC = meshgen.ef_contacts(mesh, n)
     ee, eeC = meshgen.ee_contacts(mesh, n)
     vf, vfC = meshgen.vf_contacts(mesh, n)
-    P = mas_amd.SeSchwarzPreconditioner(max_levels=L, keep_blocks=True)
+    P = mas_amd.SeSchwarzPreconditioner(max_levels=L, keep_blocks=True, reference_formation=True)
     P.m_positions, P.m_neighbours, P.m_edges, P.m_faces = mesh.pos, (mesh.starts, mesh.idx), mesh.edges, mesh.faces
     P.AllocatePrecoditioner(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0])
     P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, ef, ee, vf, efC, eeC, vfC)
@@ -257,6 +277,8 @@ def test_4m_tet_parity():
     compare_maps(P, o, mesh.nV)
     r = meshgen.residual(mesh.nV, 0x5EED + 4)
     assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
+    del P
+    _z_default_formation(mesh, cfg["levels"], o, 0x5EED + 4)
 
 
 def test_device_resident_contact_records():

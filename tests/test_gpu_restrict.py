@@ -81,3 +81,42 @@ def test_residual_hierarchy_1m_contacts():
     o.allocate(mesh)
     o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
     _check(P, o, meshgen.residual(mesh.nV, 0x5EED))
+
+
+def test_level3_handoff_across_xcds_4m_tet():
+    """The level-3 hand-off between workgroups (deep_fold.h: each node's R
+    published with write-through agent-scope stores, drained, then an
+    agent-scope arrival count; the block's last node reads the others' R with
+    agent-scope loads) at the size with the most level-3 blocks: 574 level-3
+    nodes in 18 blocks, their workgroups spread over all 8 XCDs.  R of every
+    level bitwise vs the oracle for a random and a smooth residual (where the
+    level-3 share of z is largest), and z after a previous apply with another
+    residual bitwise equal to a fresh handle's (a stale R from the previous
+    apply, or from another XCD's L2, would change Z3 and hence z)."""
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    from oracle import Oracle
+    mesh, cfg = meshgen.build_config("4M-tet")
+    P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"])
+    inf = P.info()
+    assert int(inf["level_size"][3][0]) == 574
+    o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], cfg["levels"], 16)
+    o.allocate(mesh)
+    o.prepare(mesh)
+    r_rand = meshgen.residual(mesh.nV, 77)
+    r_smooth = np.zeros_like(r_rand)
+    r_smooth[:, :3] = 1.0
+    _check(P, o, r_rand, "random")
+    _check(P, o, r_smooth, "smooth")          # P's previous apply had r_rand
+    Q = mas_amd.from_mesh(mesh, max_levels=cfg["levels"])
+    z = []
+    for H in (P, Q):
+        rd = torch.from_numpy(r_smooth).cuda()
+        zd = torch.zeros_like(rd)
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        H.PreconditioningDevice(zd, rd, s.cuda_stream)
+        s.synchronize()
+        z.append(zd.cpu().numpy())
+    np.testing.assert_array_equal(z[0], z[1])
