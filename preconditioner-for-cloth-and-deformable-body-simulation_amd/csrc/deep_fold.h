@@ -59,12 +59,12 @@ constexpr int kDeepChunk = 2048;  // list entries staged per step (8 per thread)
 // last arriving node solves the block.  The whole workgroup (kApplyThreads)
 // runs it.  List p of node T: T * stride + i.  INDEXED (the per-level form and
 // the sharded apply): d.src[d.idx[p]] (-1: padding); else d.src[p] (deepR1).
-template <bool INDEXED, bool PREFETCH = true>
+template <bool INDEXED, bool PREFETCH = true, int THREADS = kApplyThreads>
 __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int node, const DeepArgs& d,
                                           float4* __restrict__ rc, float4* __restrict__ zc, int begin1) {
     __shared__ __attribute__((aligned(16))) float st[3][kDeepChunk];  // b128 reads: 16-byte aligned rows
     __shared__ int last;
-    constexpr int kPer = kDeepChunk / kApplyThreads;
+    constexpr int kPer = kDeepChunk / THREADS;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int T = node - d.lv3Begin, blk = node >> 5;
     [[maybe_unused]] const int pw = blockIdx.x * 4 + w;  // probe slot (k_solve123 grid order)
@@ -76,7 +76,7 @@ __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int no
     auto load = [&](int b) {
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
-            const int i = b + t + kApplyThreads * q;
+            const int i = b + t + THREADS * q;
             v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (i < len) {
                 if (INDEXED) {
@@ -99,7 +99,7 @@ __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int no
         if (b0 > 0) __syncthreads();  // the previous step's fold is done with st
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
-            const int i = t + kApplyThreads * q;
+            const int i = t + THREADS * q;
             st[0][i] = v[q].x;
             st[1][i] = v[q].y;
             st[2][i] = v[q].z;

@@ -367,7 +367,8 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
     if (ev) hipEventRecord(ev[0], s);
     // coarse levels (mas_internal.h coarseMode); both forms bitwise equal
-    if (h->L > 2 && h->coarseMode == 2) launch_coarse_twopass(h, d_r, s);
+    if (h->L > 2 && h->coarseMode == 3 && coarse1_supported(h)) launch_coarse_one(h, d_r, s);
+    else if (h->L > 2 && h->coarseMode == 2) launch_coarse_twopass(h, d_r, s);
     else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
     if (ev) hipEventRecord(ev[1], s);
     launch_fine(h, 0, h->nFineBlk, d_r, d_z, s, h->applyDone, h->applyRzPart);
@@ -400,7 +401,8 @@ int build_l1src(mas_context* h, hipStream_t s) {
     k_l1src<<<cdiv((long long)n1Pad * 32, 256), 256, 0, s>>>(n1Pad, n1, P<int2>(h->members), P<int>(h->s2o),
                                                              P<int>(h->l1src));
     if ((rc = hip_check(h, hipGetLastError(), "l1src"))) return rc;
-    return build_deep_lists(h, s);  // level 3 (L >= 4)
+    if ((rc = build_deep_lists(h, s))) return rc;  // level 3 (L >= 4)
+    return build_coarse1_tables(h, s);
 }
 
 // Apply-side tables, built once per Prepare (and by mas_load_blob from the

@@ -214,13 +214,15 @@ __device__ __forceinline__ void solve12_wave(const float4* __restrict__ inv, flo
 // PREFETCH (deep_node): the level-3 block's inverse in flight during the fold
 // (182 VGPRs, 2 waves per SIMD); without it more waves per SIMD for the
 // level-1 and level-2 solves, which matters once they take several rounds.
-template <bool PREFETCH>
-__global__ __launch_bounds__(kApplyThreads) void k_solve123(const float4* __restrict__ inv, DeepArgs d,
-                                                           float4* __restrict__ rc, float4* __restrict__ zc,
-                                                           Solve12 q, const int* __restrict__ done) {
+// THREADS = 512 (the wide form): with > 128 VGPRs per wave a workgroup
+// then fills its CU, so a level-3 fold has its CU to itself.
+template <bool PREFETCH, int THREADS = kApplyThreads>
+__global__ __launch_bounds__(THREADS) void k_solve123(const float4* __restrict__ inv, DeepArgs d,
+                                                     float4* __restrict__ rc, float4* __restrict__ zc,
+                                                     Solve12 q, const int* __restrict__ done) {
     if (done && *done) return;
     if ((int)blockIdx.x < q.nDeepNodes) {  // workgroup-uniform
-        deep_node<false, PREFETCH>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, q.begin1);
+        deep_node<false, PREFETCH, THREADS>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, q.begin1);
         return;
     }
     // The level-1/2 solves have slack (~4 us of work beside the ~11 us
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_solve123(const float4* __rest
     // fold's SIMDs stay quiet.  pre-fine 21.7 -> 19.4 us at 1M + contacts
     // (sleep 32 / 64 / 127: 19.9 / 19.4 / 19.9 us).
     if (q.nDeepNodes > 0) __builtin_amdgcn_s_sleep(64);
-    const int w = (blockIdx.x - q.nDeepNodes) * (kApplyThreads / 64) + (threadIdx.x >> 6);
+    const int w = (blockIdx.x - q.nDeepNodes) * (THREADS / 64) + (threadIdx.x >> 6);
     if (w >= q.nb1 + q.nb2) return;  // wave-uniform
     solve12_wave(inv, rc, zc, q, w);
 }
@@ -348,6 +350,9 @@ void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
     else if (occ)
         k_solve123<false><<<sg, kApplyThreads, 0, s>>>(P<float4>(h->inv), d, P<float4>(h->Rc), P<float4>(h->Zc), q,
                                                        h->applyDone);
+    else if (h->coarseWide > 0)
+        k_solve123<true, 512><<<q.nDeepNodes + cdiv(q.nb1 + q.nb2, 8), 512, 0, s>>>(
+            P<float4>(h->inv), d, P<float4>(h->Rc), P<float4>(h->Zc), q, h->applyDone);
     else
         k_solve123<true><<<sg, kApplyThreads, 0, s>>>(P<float4>(h->inv), d, P<float4>(h->Rc), P<float4>(h->Zc), q,
                                                       h->applyDone);

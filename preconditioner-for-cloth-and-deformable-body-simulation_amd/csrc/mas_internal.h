@@ -115,7 +115,8 @@ struct mas_context {
     // formation (not bitwise, the default; mas_config.reference_formation = 1
     // selects 4); 0 = LDS-row k_factor
     int factorVariant = 5;
-    // coarse levels (env MAS_COARSE_MODE): 2 = two launches, restrictions then
+    // coarse levels (env MAS_COARSE_MODE): 3 = one launch (k_coarse1.hip, L >= 3);
+    // 2 = two launches, restrictions then
     // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (One-launch
     // forms and the side-stream overlap were measured slower: DESIGN.md
     // section 4.)
@@ -124,6 +125,8 @@ struct mas_context {
     // level-1 level has >= kCoarseOccBlocks blocks, 0 = never, 1 = always;
     // env MAS_COARSE_OCC
     int coarseOcc = -1;
+    int coarseWide = 0;
+    int c1EarlyInv = 0;     // k_coarse1 bank waves: level-1 inverse loaded with the gathers (env MAS_C1_EARLY_INV)     // k_solve123 in 512-thread workgroups (env MAS_COARSE_WIDE)
     int coarseNarrow = -1;  // single-wave coarse workgroups: -1 = at L = 3, 0 = never, 1 = always (env MAS_COARSE_NARROW)
     // fine kernel (env MAS_FINE_VARIANT, k_apply.hip): 1 = nontemporal inverse
     // loads (4-wave workgroups); 3 = the same in one-wave workgroups (A/B);
@@ -166,6 +169,9 @@ struct mas_context {
     // every level-1 node, R1 in list order (deepR1), per-block arrival counters
     mas::Buffer deepKeys, deepVals, deepIdx, deepOff, deepPos, deepR1, deepCnt, deepIdxShard;
     int deepStride = 0;  // list slots per level-3 node (the longest list, rounded up to 4)
+    // one-launch coarse form (k_coarse1.hip): per level-2 block the arrival
+    // counters, then the expected arrival counts (2 x ceil(n2 / 32) ints)
+    mas::Buffer l2Cnt, l1info;
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
     mas::Buffer pcgRzPart;                               // PCG: r.z partials of the fine apply kernel
@@ -209,7 +215,7 @@ struct mas_context {
                               &vlist, &voff, &tab, &termCnt, &termOff, &terms,
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cFineVal, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
-                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &l2Cnt, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -250,6 +256,9 @@ int upload_slot_table(mas_context* h);
 int prepare_apply_tables(mas_context* h, hipStream_t s);
 int build_l1src(mas_context* h, hipStream_t s);
 void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s);
+void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s);  // k_coarse1.hip (L >= 3)
+int build_coarse1_tables(mas_context* h, hipStream_t s);
+bool coarse1_supported(const mas_context* h);  // every level-3 list fits a fold wave (k_coarse1.hip)
 void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
 void launch_coarse_deep(mas_context* h, const float4* src, const int* idx, hipStream_t s);
 int deep_nodes(const mas_context* h);  // level-3 node ids incl. padding (0 below L = 4)

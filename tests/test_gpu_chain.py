@@ -1,5 +1,6 @@
-"""The two-pass coarse launch form (k_coarse.hip, the default), in both of
-its forms, against one launch per coarse level (k_apply.hip).
+"""The one-launch coarse form (k_coarse1.hip) and the two-pass form
+(k_coarse.hip), in both of its forms, against one launch per coarse level
+(k_apply.hip).
 
 Every sum runs in the same order in both forms, so the bar is BITWISE
 equality, per apply, over many back-to-back applies with a different residual
@@ -15,14 +16,15 @@ pytestmark = pytest.mark.gpu
 
 
 def _handles(mesh, L, contacts, monkeypatch):
-    """Per-level (mode 0), two-pass (2) and two-pass in its occupancy form
-    (the default from 4 096 level-1 blocks: SoA restriction staging, no
-    level-3 inverse prefetch) handles."""
+    """Per-level (mode 0), two-pass (2), two-pass in its occupancy form
+    (SoA restriction staging, no level-3 inverse prefetch) and one-launch (3)
+    handles."""
     import mas_amd
     hs = []
-    for mode, occ in ((0, 0), (2, 0), (2, 1)):
+    for mode, occ, wide in ((0, 0, 0), (2, 0, 0), (2, 1, 0), (3, 0, 0), (2, 0, 1)):
         monkeypatch.setenv("MAS_COARSE_MODE", str(mode))
         monkeypatch.setenv("MAS_COARSE_OCC", str(occ))
+        monkeypatch.setenv("MAS_COARSE_WIDE", str(wide))
         hs.append(mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts))
         assert hs[-1].stats()["apply_mode"] == mode
     return hs
@@ -40,7 +42,7 @@ def _applies(P, rs, stream):
 
 CASES = [("cloth", 20, 0, 0), ("cloth", 40, 2, 0), ("cloth", 100, 3, 0), ("cloth", 100, 0, 500),
          ("cloth", 33, 0, 0), ("tet", 16, 3, 0), ("tet", 12, 0, 0), ("cloth", 256, 4, 2000),
-         ("cloth", 512, 3, 0), ("cloth", 512, 5, 0)]
+         ("cloth", 512, 3, 0), ("cloth", 512, 5, 0), ("tet", 48, 4, 0)]
 
 
 @pytest.mark.parametrize("kind,W,L,nc", CASES)
@@ -49,11 +51,11 @@ def test_twopass_equals_per_level(kind, W, L, nc, monkeypatch):
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=11) if nc else None
-    P3, P2, P2o = _handles(mesh, L, contacts, monkeypatch)
+    P3, P2, P2o, P1, P2w = _handles(mesh, L, contacts, monkeypatch)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 100 + k)).cuda() for k in range(24)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    for PX in (P2, P2o):
+    for PX in (P2, P2o, P1, P2w):
         zf = _applies(PX, rs, s)
         for k, (a, b) in enumerate(zip(zf, z3)):
             np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
@@ -71,11 +73,11 @@ def test_twopass_1m_contacts_bitwise_and_oracle(monkeypatch):
     from oracle import Oracle
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    P3, P2, P2o = _handles(mesh, 4, contacts, monkeypatch)
+    P3, P2, P2o, P1, P2w = _handles(mesh, 4, contacts, monkeypatch)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 0x5EED + k)).cuda() for k in range(40)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    for PX in (P2, P2o):
+    for PX in (P2, P2o, P1, P2w):
         zf = _applies(PX, rs, s)
         for k, (a, b) in enumerate(zip(zf, z3)):
             np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")

@@ -49,7 +49,7 @@ def _check(P, o, r, tag=""):
 
 @pytest.mark.parametrize("kind,W,L,nc", [("cloth", 100, 4, 0), ("cloth", 256, 4, 2000), ("cloth", 512, 5, 0),
                                          ("tet", 16, 4, 0), ("cloth", 64, 3, 0)])
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 2, 3])
 def test_residual_hierarchy_bitwise(kind, W, L, nc, mode, monkeypatch):
     import mas_amd
     from mas_amd import meshgen
