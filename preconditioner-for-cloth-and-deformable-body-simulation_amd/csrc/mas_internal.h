@@ -125,8 +125,7 @@ struct mas_context {
     // level-1 level has >= kCoarseOccBlocks blocks, 0 = never, 1 = always;
     // env MAS_COARSE_OCC
     int coarseOcc = -1;
-    int coarseWide = 0;
-    int c1EarlyInv = 0;     // k_coarse1 bank waves: level-1 inverse loaded with the gathers (env MAS_C1_EARLY_INV)     // k_solve123 in 512-thread workgroups (env MAS_COARSE_WIDE)
+    int coarseWide = 0;     // k_solve123 in 512-thread workgroups (env MAS_COARSE_WIDE)
     int coarseNarrow = -1;  // single-wave coarse workgroups: -1 = at L = 3, 0 = never, 1 = always (env MAS_COARSE_NARROW)
     // fine kernel (env MAS_FINE_VARIANT, k_apply.hip): 1 = nontemporal inverse
     // loads (4-wave workgroups); 3 = the same in one-wave workgroups (A/B);
