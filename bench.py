@@ -103,18 +103,44 @@ def cpu_info():
             "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"), "OMP_PLACES": os.environ.get("OMP_PLACES")}
 
 
+def cgroup_cpus():
+    """CPUs the cgroup quota allows this process (None: no quota)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:          # cgroup v2: "<quota> <period>" or "max <period>"
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:                                                   # cgroup v1
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return max(1, -(-q // per)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(mesh, cfg, contacts, r_np, steps):
     """OMP_NUM_THREADS = CPU_THREAD_NUM = nproc - 1 (the reference's
-    WIN32 rule, SeOmp.cpp:29-33), threads pinned close.  The box's own
-    OMP_NUM_THREADS (a CPU-share hint) is timed beside it when it differs."""
+    WIN32 rule, SeOmp.cpp:29-33), threads pinned close, where nproc is the number
+    of CPUs this process may run on: its affinity set, capped by the cgroup CPU
+    quota when there is one (the GPU box shows the whole host's 256 CPUs but
+    grants a share of them; 255 threads on that share measured ~40x slower).
+    The raw nproc - 1 and the box's OMP_NUM_THREADS are timed beside it (shorter
+    samples) when they differ."""
     os.environ["OMP_PROC_BIND"] = "close"   # before the OpenMP runtime loads
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from oracle import Oracle  # test infrastructure: the timed CPU baseline only
     try:
-        ncpu = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        ncpu = os.cpu_count() or 2
-    threads = max(1, ncpu - 1)
+        affinity = os.cpu_count() or 2
+    quota = cgroup_cpus()
+    avail = min(affinity, quota) if quota else affinity
+    threads = max(1, avail - 1)
     env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], cfg["levels"], threads)
     o.allocate(mesh)
@@ -123,27 +149,32 @@ def cpu_baseline(mesh, cfg, contacts, r_np, steps):
     else:
         o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
 
-    def timed(n):
+    def timed(n, k):
         o.set_threads(n)
         for _ in range(3):
             o.apply(r_np)
         ts = []
-        for _ in range(steps):
+        for _ in range(k):
             t = time.perf_counter()
             z = o.apply(r_np)
             ts.append(time.perf_counter() - t)
         return statistics.median(ts), z
 
-    med, z = timed(threads)
+    med, z = timed(threads, steps)
     out = {"value": round(1.0 / med, 3), "unit": "applies/s", "cores": threads, "kind": "port", **cpu_info(),
-           "OMP_NUM_THREADS_env": env_threads or None,
-           "sample": f"{cfg['name']} workload, oracle/ CPU restatement (OpenMP, {threads} threads = nproc - 1, "
-                     f"OMP_PROC_BIND=close, reference packed layout), median of {steps} applies after 3 warm-up; "
-                     f"ms/apply {med * 1e3:.2f}"}
+           "cgroup_quota_cpus": quota, "OMP_NUM_THREADS_env": env_threads or None,
+           "sample": f"{cfg['name']} workload, oracle/ CPU restatement (OpenMP, {threads} threads = nproc - 1 "
+                     f"with nproc = {avail} CPUs available to the process, OMP_PROC_BIND=close, reference "
+                     f"packed layout), median of {steps} applies after 3 warm-up; ms/apply {med * 1e3:.2f}"}
+    others = {}
     if env_threads and env_threads != threads:
-        med2, _ = timed(env_threads)
-        out["at_OMP_NUM_THREADS_env"] = {"threads": env_threads, "value": round(1.0 / med2, 3),
-                                         "ms_per_apply": round(med2 * 1e3, 3)}
+        others["at_OMP_NUM_THREADS_env"] = env_threads
+    raw = max(1, (os.cpu_count() or 2) - 1)
+    if raw != threads:
+        others["at_raw_nproc_minus_1"] = raw
+    for key, n in others.items():
+        m2, _ = timed(n, max(3, steps // 4))
+        out[key] = {"threads": n, "value": round(1.0 / m2, 3), "ms_per_apply": round(m2 * 1e3, 3)}
     return out, z
 
 

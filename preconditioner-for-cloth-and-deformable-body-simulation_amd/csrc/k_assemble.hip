@@ -389,6 +389,61 @@ __global__ __launch_bounds__(256) void k_od(FineAsm a, float* __restrict__ od, i
     recCnt[v] = cnt;
 }
 
+// k_od with G lanes per vertex (G >= the largest neighbour count): lane j
+// loads ELL slot 1 + j's block (when it is a same-bank neighbour) so every
+// load of a vertex is in flight at once -- the thread-per-vertex form waits a
+// dependent chain per 4 slots (217 us at 1M + contacts, ~1.3 TB/s).  The
+// blocks go through LDS, then lane q of the vertex's group folds entry q over
+// the slots in ELL order (the same left fold, skipping cross-bank slots:
+// bitwise equal to k_od).
+template <int G>
+__global__ __launch_bounds__(256) void k_od_lanes(FineAsm a, float* __restrict__ od, int* __restrict__ recCnt) {
+    constexpr int VPW = 64 / G;  // vertices per wave
+    __shared__ float stg[4][64][10];  // [wave][lane][entry], padded row
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int v = t / G, j = t % G, g0 = lane & ~(G - 1);
+    const bool vin = v < a.nV;
+    int o = 0, num = 0;
+    if (vin) {
+        o = a.s2o[v];
+        num = a.nbrNum[v];
+    }
+    const int k = 1 + j;
+    const unsigned ot = vin && k < num ? (unsigned)a.nbr[(size_t)k * a.nV + v] : 0xffffffffu;
+    const bool has = vin && k < num;
+    const bool same = has && (ot >> 5) == ((unsigned)v >> 5);
+    const unsigned long long bs = __ballot(has && !same);
+    if (vin && j == 0) recCnt[v] = __popcll((bs >> g0) & (G == 64 ? ~0ull : ((1ull << G) - 1)));
+    float m[9];
+    if (same) {
+        const float* src = a.off9 + 9 * ((size_t)a.ranges[o] + k - 1);
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) m[r * 3 + c] = src[c * 3 + r];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 9; ++q) m[q] = 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) stg[w][lane][q] = m[q];
+    stg[w][lane][9] = same ? 1.f : 0.f;
+    __syncthreads();
+    if (!vin) return;
+    // lane j folds entries j (and 8 when G = 8, lane 0) of the vertex's od
+    for (int q = j; q < 9; q += G) {
+        const int r = q / 3, c = q % 3;
+        const float* d = a.diag9 + 9 * (size_t)o;
+        const float* ad = a.additional + 9 * (size_t)v;
+        float acc = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);
+        for (int s = 0; s < G && 1 + s < num; ++s)
+            if (stg[w][g0 + s][9] != 0.f) acc = __fadd_rn(acc, stg[w][g0 + s][q]);
+        od[9 * (size_t)v + q] = acc;
+    }
+    (void)VPW;
+}
+
 // Entry keys.  A record's row and column nodes always share a bank (the
 // climb stops at the first level where they do), so an entry is its row id
 // relative to begin1 and the column's lane: key = (row - begin1) * 32 +
@@ -878,10 +933,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         (rc = exclusive_scan(h, P<int>(h->caCnt), P<int>(h->caOff), n + 1, s, "contact scan")))
         return rc;
     int tot[2] = {0, 0};
-    if ((rc = hip_check(h, hipMemcpyAsync(&tot[0], P<int>(h->cdOff) + n, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
-        (rc = hip_check(h, hipMemcpyAsync(&tot[1], P<int>(h->caOff) + n, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
-        (rc = hip_check(h, hipStreamSynchronize(s), "contact count sync")))
-        return rc;
+    if ((rc = read_back(h, s, {P<int>(h->cdOff) + n, P<int>(h->caOff) + n}, tot))) return rc;
     const int nD = tot[0], nA = tot[1];
     const size_t d1 = nD > 0 ? nD : 1, a1 = nA > 0 ? nA : 1;
     if ((rc = ensure(h, h->cdKeys, d1 * 4)) || (rc = ensure(h, h->cdKeysS, d1 * 4)) ||
@@ -904,10 +956,6 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     // fine entries: k_level0_block; coarse entries: folded onto the zeroed coarse blocks
     k_contact_fine_bounds<<<cdiv(nD + 1, 256), 256, 0, s>>>(nD, RecKey::kLaneBits, begin1, h->nFineBlk,
                                                             P<EntryKey>(h->cdKeysS), P<int>(h->cFineOff));
-    int fineEnd = 0;
-    if ((rc = hip_check(h, hipMemcpyAsync(&fineEnd, P<int>(h->cFineOff) + h->nFineBlk, 4, hipMemcpyDeviceToHost, s),
-                        "D2H")))
-        return rc;
     // additional rows (level 0 and coarse), folded from zero
     if (nA > 0)
         k_fold_runs<NodeRow, true, unsigned><<<cdiv(nA, 64), 64, 0, s>>>(
@@ -935,10 +983,9 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     }
     k_push_count<<<cdiv(nA + 1, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), gn, P<int>(h->cpCnt));
     if ((rc = exclusive_scan(h, P<int>(h->cpCnt), P<int>(h->cpOff), nA + 1, s, "push scan"))) return rc;
-    int nP = 0;
-    if ((rc = hip_check(h, hipMemcpyAsync(&nP, P<int>(h->cpOff) + nA, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
-        (rc = hip_check(h, hipStreamSynchronize(s), "push count sync")))
-        return rc;
+    int pf[2] = {0, 0};  // push count, first coarse block-entry record
+    if ((rc = read_back(h, s, {P<int>(h->cpOff) + nA, P<int>(h->cFineOff) + h->nFineBlk}, pf))) return rc;
+    const int nP = pf[0], fineEnd = pf[1];
     const RecKey rk{0, B};
     if (nD > fineEnd)
         k_fold_runs<DenseEntry, true, EntryKey><<<cdiv(nD - fineEnd, 64), 64, 0, s>>>(
@@ -994,7 +1041,13 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         // the level-0 blocks assemble and factor on prepStream while this
         // stream assembles the coarse levels (run_factor joins)
         if (!forked && (rc = fork_fused(h, fa, s))) return rc;
-        k_od<<<cdiv(nV, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+        // od and the coarse record counts; lanes per vertex: the largest
+        // neighbour count (ELL slot 0 is the vertex itself), a power of two
+        const int val = h->maxNbr - 1;
+        if (val <= 8) k_od_lanes<8><<<cdiv((long long)nV * 8, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+        else if (val <= 16) k_od_lanes<16><<<cdiv((long long)nV * 16, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+        else if (val <= 32) k_od_lanes<32><<<cdiv((long long)nV * 32, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+        else k_od<<<cdiv(nV, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
     } else {
         k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
                                                   d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt),
@@ -1011,9 +1064,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                         "record scan")))
         return rc;
     int nRec = 0;
-    if ((rc = hip_check(h, hipMemcpyAsync(&nRec, P<int>(h->recOff) + nV, 4, hipMemcpyDeviceToHost, s), "D2H nRec")) ||
-        (rc = hip_check(h, hipStreamSynchronize(s), "nRec sync")))
-        return rc;
+    if ((rc = read_back(h, s, {P<int>(h->recOff) + nV}, &nRec))) return rc;
     const size_t nr = nRec > 0 ? nRec : 1;
     if ((rc = ensure(h, h->rec, nr * sizeof(EdgeRec))) || (rc = ensure(h, h->recKeys, nr * 4)) ||
         (rc = ensure(h, h->recKeysSorted, nr * 4)) || (rc = ensure(h, h->recIds, nr * 4)) ||

@@ -431,9 +431,7 @@ int build_deep_lists(mas_context* h, hipStream_t s) {
         return rc;
     k_deep_off<<<cdiv(nDeep + 1, 256), 256, 0, s>>>(nDeep, n1, keysS, off, off + nDeep + 1);
     int maxLen = 0;
-    if ((rc = hip_check(h, hipMemcpyAsync(&maxLen, off + nDeep + 1, 4, hipMemcpyDeviceToHost, s), "D2H")) ||
-        (rc = hip_check(h, hipStreamSynchronize(s), "deep lists sync")))
-        return rc;
+    if ((rc = read_back(h, s, {off + nDeep + 1}, &maxLen))) return rc;
     const int stride = std::max(32, (maxLen + 31) / 32 * 32);  // whole 8-float4 batches in the fold
     const size_t slots = (size_t)nDeep * stride;
     if ((rc = ensure(h, h->deepIdx, slots * 4)) || (rc = ensure(h, h->deepR1, slots * 16)) ||

@@ -343,9 +343,7 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
     // deterministic compaction == the reference's atomic slot counter at CPU_THREAD_NUM=1
     if ((rc = scan_counts(h, P<int>(h->stencilFlags), slots, n + 1, s))) return rc;
     int head[2] = {0, 0};  // stencil count, bad-record word
-    if ((rc = hip_check(h, hipMemcpyAsync(head, slots + n, 8, hipMemcpyDeviceToHost, s), "D2H stencil count")) ||
-        (rc = hip_check(h, hipStreamSynchronize(s), "stencil count sync")))
-        return rc;
+    if ((rc = read_back(h, s, {slots + n, slots + n + 1}, head))) return rc;
     if (head[1]) return fail(h, MAS_ERR_ARG, "contact record references an out-of-range edge/face/vertex");
     const int valid = head[0];
     k_stencil_build<<<cdiv(n, 256), 256, 0, s>>>(raw, (int)efNum, (int)eeNum, n, P<int>(h->stencilFlags),
@@ -403,10 +401,7 @@ int run_levels(mas_context* h, hipStream_t s) {
         k_next_level<<<g, 256, 0, s>>>(nV, prev, next, cst + (size_t)level * nV);
     }
     int totals[kMaxLevels + 2] = {};
-    if ((rc = hip_check(h, hipMemcpyAsync(totals, tot, (size_t)(L + 1) * 4, hipMemcpyDeviceToHost, s),
-                        "D2H level totals")) ||
-        (rc = hip_check(h, hipStreamSynchronize(s), "level sync")))
-        return rc;
+    if ((rc = read_back(h, s, {tot, tot + 1, tot + 2, tot + 3, tot + 4, tot + 5}, totals))) return rc;
     h->levelSize[2] = totals[1];
     h->levelSize[3] = nv32;
     for (int level = 1; level < L; ++level) {

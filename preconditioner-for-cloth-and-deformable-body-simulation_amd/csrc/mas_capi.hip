@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <chrono>
 #include <new>
 
 #include "mas_internal.h"
@@ -39,6 +40,57 @@ int ensure(mas_context* h, Buffer& b, size_t bytes) {
         return fail(h, MAS_ERR_NOMEM, std::string("hipMalloc ") + std::to_string(bytes) + " B: " + hipGetErrorString(e));
     }
     b.bytes = bytes;
+    return MAS_OK;
+}
+
+// Small device -> host reads (sizes the host needs before its next
+// launches) through pinned memory: one single-lane kernel copies up to 8 ints
+// to the pinned words and then publishes a sequence number; the host spins
+// on that word.  hipStreamSynchronize + a pageable copy cost ~40 us of
+// wake-up each (7 of them per Prepare); this costs the
+// kernel's completion plus a few microseconds.  Falls back to a stream
+// synchronisation after 5 s (never spins forever).
+struct ReadBackArgs {
+    const int* src[8];
+    int n;
+};
+__global__ void k_readback(ReadBackArgs a, int* host, int seq) {
+    if (threadIdx.x != 0) return;
+    int v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = i < a.n ? *a.src[i] : 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (i < a.n) __hip_atomic_store(host + 1 + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* out) {
+    if (src.size() > 8) return fail(h, MAS_ERR_ARG, "read_back: at most 8 words");
+    if (!h->rbHost) {
+        void* p = nullptr;
+        int rc = hip_check(h, hipHostMalloc(&p, 16 * sizeof(int), hipHostMallocCoherent), "pinned read-back words");
+        if (rc) return rc;
+        h->rbHost = static_cast<int*>(p);
+        std::memset(p, 0, 16 * sizeof(int));
+    }
+    ReadBackArgs a{};
+    a.n = (int)src.size();
+    int i = 0;
+    for (const int* p : src) a.src[i++] = p;
+    const int seq = ++h->rbSeq;
+    k_readback<<<1, 64, 0, s>>>(a, h->rbHost, seq);
+    int rc = hip_check(h, hipGetLastError(), "read-back kernel");
+    if (rc) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(h->rbHost, __ATOMIC_ACQUIRE) != seq) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+            if ((rc = hip_check(h, hipStreamSynchronize(s), "read-back sync"))) return rc;
+            if (__atomic_load_n(h->rbHost, __ATOMIC_ACQUIRE) != seq) return fail(h, MAS_ERR_HIP, "read-back lost");
+            break;
+        }
+    }
+    for (int k = 0; k < a.n; ++k) out[k] = __atomic_load_n(h->rbHost + 1 + k, __ATOMIC_RELAXED);
     return MAS_OK;
 }
 
@@ -135,6 +187,7 @@ int mas_destroy(mas_handle h) {
     if (h->evGathered) hipEventDestroy(h->evGathered);
     if (h->evShardDone) hipEventDestroy(h->evShardDone);
     if (h->stream) hipStreamDestroy(h->stream);
+    if (h->rbHost) hipHostFree(h->rbHost);
     delete h;
     return MAS_OK;
 }

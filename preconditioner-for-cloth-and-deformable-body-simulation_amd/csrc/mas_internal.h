@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -193,6 +194,9 @@ struct mas_context {
     void* rcclComm = nullptr;  // ncclComm_t (comm_rccl.hip)
     int rcclRank = -1, rcclWorld = 0;
     hipEvent_t* shardPendingEv = nullptr;  // profiling events of an overlapped sharded apply in flight
+    // pinned words of read_back (small device -> host reads), their sequence
+    int* rbHost = nullptr;
+    int rbSeq = 0;
     // staging for host-pointer entry points
     mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
     // hipcub scratch
@@ -273,6 +277,8 @@ void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float
 void launch_prolong(mas_context* h, int v0, int v1, float4* z, hipStream_t s);
 int fine_grid(const mas_context* h);  // workgroups of one fine launch over every level-0 block
 int compute_l1_first(mas_context* h, hipStream_t s);
+// up to 8 device ints -> out, through pinned memory (mas_capi.hip)
+int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* out);
 void release_comm(mas_context* h);  // comm_rccl.hip
 int copy_block_inverse(mas_context* h, int blk, float* out96);
 int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,

@@ -1,6 +1,6 @@
-# Full GPU tests, then steady-state Prepare timings: bash scripts/dev/gpu_prep_check.sh <out>
+# Prepare changes: parity tests that check every assembled block bitwise, then steady-state Prepare times
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-prepcheck}; mkdir -p $O; export TMPDIR=/tmp; cd $R
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
-tail -1 $O/pytest_gpu.log
-for cfg in 1M+contacts 4M-tet; do echo $cfg; timeout -k 10 100 python scripts/dev/prep_only.py $cfg 3 2>&1 | grep prepare || exit 1; done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_blob.py tests/test_gpu_shard.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 && \
+for c in 1M+contacts 1M 256k 4M-tet; do timeout -k 10 200 python scripts/dev/prep_only.py $c 4 > $O/prep_$c.log 2>&1 || exit 1; done
+echo "exit $?"

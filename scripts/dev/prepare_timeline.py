@@ -9,7 +9,8 @@ name contains the last substring (default k_factor_rb).
 import csv
 import sys
 
-rows = list(csv.DictReader(open(f"{sys.argv[1]}/trace/run_kernel_trace.csv")))
+import glob
+rows = list(csv.DictReader(open(glob.glob(f"{sys.argv[1]}/**/run_kernel_trace.csv", recursive=True)[0])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 first = sys.argv[2] if len(sys.argv) > 2 else "k_stencil_flags"
 last = sys.argv[3] if len(sys.argv) > 3 else "k_factor_rb"
