@@ -298,6 +298,13 @@ int mas_get_block_inverse(mas_handle h, int blk, float* out96x96);
  * level is never prolonged, CollectFinalZ .cpp:1706-1717, so it is skipped),
  * where the reference's m_mappedR holds the sums. */
 int mas_get_coarse_residual(mas_handle h, float* out4);
+/* Diagnostics of Prepare's building blocks on device buffers (tests): the
+ * stable pair sort by the low `bits` key bits and the int exclusive scan, on
+ * the handle's stream, synchronised before return.  impl 1 = the library's
+ * look-back-free kernels (rsort.hip), 0 = rocprim/hipcub. */
+int mas_dev_sort_pairs(mas_handle h, const unsigned* d_keys_in, unsigned* d_keys_out, const int* d_vals_in,
+                       int* d_vals_out, int n, int bits, int impl);
+int mas_dev_exclusive_scan(mas_handle h, const int* d_in, int* d_out, int n, int impl);
 
 #ifdef __cplusplus
 }

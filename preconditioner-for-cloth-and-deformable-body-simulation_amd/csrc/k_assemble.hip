@@ -873,6 +873,8 @@ __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, 
 
 template <class T>
 static int exclusive_scan(mas_context* h, const T* in, T* out, int n, hipStream_t s, const char* what) {
+    if constexpr (std::is_same_v<T, int>)
+        if (h->sortImpl) return rs_exclusive_scan(h, in, out, n, s, what);
     size_t tmp = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, n, s);
     int rc = ensure(h, h->cubTemp, tmp);
@@ -1056,13 +1058,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     if (L == 1) return hip_check(h, hipGetLastError(), "assembly kernels");
 
     // coarse edge records in (u, k) order
-    size_t tmp = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, P<int>(h->recCnt), P<int>(h->recOff), nV + 1, s);
-    if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
-    if ((rc = hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, P<int>(h->recCnt), P<int>(h->recOff),
-                                                            nV + 1, s),
-                        "record scan")))
-        return rc;
+    if ((rc = exclusive_scan(h, P<int>(h->recCnt), P<int>(h->recOff), nV + 1, s, "record scan"))) return rc;
     int nRec = 0;
     if ((rc = read_back(h, s, {P<int>(h->recOff) + nV}, &nRec))) return rc;
     const size_t nr = nRec > 0 ? nRec : 1;
@@ -1121,13 +1117,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         k_bounds<<<cdiv(nV, 256), 256, 0, s>>>(nV, P<int>(h->vkeys), count, P<int>(h->voff));
         k_term_count<<<cdiv(nV + 1, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff), rec,
                                                        P<int>(h->termCnt));
-        tmp = 0;
-        hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, P<int>(h->termCnt), P<int>(h->termOff), nV + 1, s);
-        if ((rc = ensure(h, h->cubTemp, tmp))) return rc;
-        if ((rc = hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, P<int>(h->termCnt),
-                                                                P<int>(h->termOff), nV + 1, s),
-                            "term scan")))
-            return rc;
+        if ((rc = exclusive_scan(h, P<int>(h->termCnt), P<int>(h->termOff), nV + 1, s, "term scan"))) return rc;
         switch (lanesPerVertex) {
             case 8:
                 k_term_write<<<cdiv(nV, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff), rec,

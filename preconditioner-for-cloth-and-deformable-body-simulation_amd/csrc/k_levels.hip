@@ -279,6 +279,7 @@ __global__ __launch_bounds__(256) void k_vertex_maps(int nV, int L, const int* _
 // ---------------------------------------------------------------------------
 
 static int scan_counts(mas_context* h, const int* counts, int* prefix, int n, hipStream_t s) {
+    if (h->sortImpl) return rs_exclusive_scan(h, counts, prefix, n, s, "exclusive scan");
     size_t tmp = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, counts, prefix, n, s);
     int rc = ensure(h, h->cubTemp, tmp);

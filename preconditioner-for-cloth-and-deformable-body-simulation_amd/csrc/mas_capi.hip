@@ -11,6 +11,8 @@
 #include <chrono>
 #include <new>
 
+#include <hipcub/hipcub.hpp>
+
 #include "mas_internal.h"
 
 namespace mas {
@@ -145,6 +147,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_COARSE_OCC")) h->coarseOcc = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_NARROW")) h->coarseNarrow = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_WIDE")) h->coarseWide = std::atoi(v);
+    if (const char* v = std::getenv("MAS_SORT")) h->sortImpl = std::atoi(v);
     if (h->cfg.reference_formation) h->factorVariant = 4;
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
@@ -467,3 +470,32 @@ int mas_set_prepare_shard(mas_handle h, int rank, int world) {
 }
 
 }  // extern "C"
+
+int mas_dev_sort_pairs(mas_handle h, const unsigned* d_keys_in, unsigned* d_keys_out, const int* d_vals_in,
+                       int* d_vals_out, int n, int bits, int impl) {
+    if (!h || n < 0 || (n > 0 && (!d_keys_in || !d_keys_out || !d_vals_in || !d_vals_out))) return MAS_ERR_ARG;
+    hipSetDevice(h->device);
+    const int keep = h->sortImpl;
+    h->sortImpl = impl;
+    const int rc = mas::sort_pairs_u32(h, d_keys_in, d_keys_out, d_vals_in, d_vals_out, n, bits, h->stream, "sort");
+    h->sortImpl = keep;
+    if (rc) return rc;
+    return hip_check(h, hipStreamSynchronize(h->stream), "sort");
+}
+
+int mas_dev_exclusive_scan(mas_handle h, const int* d_in, int* d_out, int n, int impl) {
+    if (!h || n < 0 || (n > 0 && (!d_in || !d_out))) return MAS_ERR_ARG;
+    hipSetDevice(h->device);
+    int rc;
+    if (impl) {
+        rc = mas::rs_exclusive_scan(h, d_in, d_out, n, h->stream, "scan");
+    } else {
+        size_t tmp = 0;
+        hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_in, d_out, n, h->stream);
+        rc = ensure(h, h->cubTemp, tmp);
+        if (!rc)
+            rc = hip_check(h, hipcub::DeviceScan::ExclusiveSum(h->cubTemp.p, tmp, d_in, d_out, n, h->stream), "scan");
+    }
+    if (rc) return rc;
+    return hip_check(h, hipStreamSynchronize(h->stream), "scan");
+}

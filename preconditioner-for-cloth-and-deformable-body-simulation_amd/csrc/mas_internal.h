@@ -201,6 +201,10 @@ struct mas_context {
     mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
     // hipcub scratch
     mas::Buffer cubTemp;
+    // look-back-free radix sort and scan (rsort.hip): ping-pong keys/values,
+    // per-tile digit counts, scan tile sums; env MAS_SORT=0 selects rocprim (A/B)
+    mas::Buffer rsKeys, rsVals, rsHist, rsPart;
+    int sortImpl = 1;
     // events: [0..1] allocate, [2..3] prepare
     hipEvent_t ev[4] = {};
     // profiling ring: 4 events per apply (start, restrict end, coarse end, fine end)
@@ -219,7 +223,7 @@ struct mas_context {
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cFineVal, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
                               &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &l2Cnt, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
-                              &cubTemp};
+                              &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart};
         for (mas::Buffer* b : all) f(*b);
     }
 };
@@ -268,6 +272,10 @@ int deep_nodes(const mas_context* h);  // level-3 node ids incl. padding (0 belo
 mas::DeepArgs deep_args(mas_context* h, const float4* src, const int* idx);
 int build_deep_lists(mas_context* h, hipStream_t s);
 int build_deep_shard_idx(mas_context* h, hipStream_t s);
+// rsort.hip: stable sort by the low `bits` key bits; exclusive scan
+int rs_sort_pairs(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
+                  hipStream_t s, const char* what);
+int rs_exclusive_scan(mas_context* h, const int* in, int* out, int n, hipStream_t s, const char* what);
 int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
                    hipStream_t s, const char* what);
 // level-0 blocks [blk0, blkEnd) + prolongation; done / rzPart: PCG hooks (k_apply.hip)

@@ -41,7 +41,7 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
            "mas_apply_shard_fine", "mas_apply_shard_complete", "mas_shard_apply_device", "mas_rccl_unique_id",
            "mas_rccl_init", "mas_shard_apply_rccl",
            "mas_pcg_solve_device", "mas_pcg_solve", "mas_blob_size", "mas_save_blob", "mas_load_blob",
-           "mas_blob_validate"]
+           "mas_blob_validate", "mas_dev_sort_pairs", "mas_dev_exclusive_scan"]
 
 
 class mas_config(ctypes.Structure):
@@ -136,6 +136,8 @@ def lib():
         L.mas_rccl_unique_id.argtypes = [P]
         L.mas_rccl_init.argtypes = [P, P, I, I]
         L.mas_shard_apply_rccl.argtypes = [P, P, P, P]
+        L.mas_dev_sort_pairs.argtypes = [P, P, P, P, P, I, I, I]
+        L.mas_dev_exclusive_scan.argtypes = [P, P, P, I, I]
         F = ctypes.c_float
         L.mas_pcg_solve_device.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result), P]
         L.mas_pcg_solve.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result)]
