@@ -3,8 +3,12 @@
  * (V-Sekai/preconditioner-for-cloth-and-deformable-body-simulation,
  * SeSchwarzPreconditioner.cpp).  TEST INFRASTRUCTURE ONLY -- see mas_oracle.h.
  *
- * Parity: PARTIALLY PINNED (reference unbuildable here; pinned against the
- * reference-run known answers in SURVEY.md and numpy fp64 checks).
+ * Parity: PARTIALLY PINNED.  Morton codes, Clamp and the value layouts are
+ * pinned against the reference's own unmodified headers (oracle/ref_headers.cpp,
+ * tests/test_ref_pinned.py); level sizes / block counts against reference runs
+ * recorded in SURVEY.md; the .cpp's floating-point phases are unpinned (the
+ * .cpp needs MSVC headers and a source patch) and checked by numpy fp64
+ * identities.
  *
  * Policy on the reference's defects:
  *   B-1 sort only on the first Allocate (reproduced; orc_allocate re-sorts only

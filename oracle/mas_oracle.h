@@ -5,13 +5,16 @@
  * cpu_baseline leg of bench.py may load this library, and only as the checker
  * (or the timed CPU baseline).  The product (libmas_amd.so) never links it.
  *
- * Parity status: PARTIALLY PINNED.  The reference (SeSchwarzPreconditioner.cpp)
- * cannot be built in this image without stand-ins for MSVC headers and a source
- * patch (see DESIGN.md "Oracle"), and it ships no tests or golden vectors.  This
- * restatement is pinned against the reference-run known answers recorded in
- * SURVEY.md (level sizes, active block counts, PCG iteration counts; see
- * tests/golden/known_answers.json) and against independent numpy fp64 checks
- * (Galerkin coarse blocks, exact local solves).
+ * Parity status: PARTIALLY PINNED.  The reference's .cpp cannot be built in
+ * this image without stand-ins for MSVC headers and a source patch (DESIGN.md
+ * section 2), and it ships no tests or golden vectors.  Its headers do build
+ * unmodified: Morton codes, Math::Clamp and the value layouts are pinned against
+ * them (oracle/ref_headers.cpp -> tests/golden/ref_headers.json,
+ * ref_morton.npz).  Level sizes, active block counts and PCG iteration counts
+ * are pinned against reference runs recorded in SURVEY.md
+ * (tests/golden/known_answers.json); the floating-point phases are unpinned and
+ * checked by independent numpy fp64 identities (Galerkin coarse blocks, exact
+ * local solves).
  *
  * Every function cites the reference file:line it restates.  Buffer layouts
  * follow the reference: float4 vectors (SeVec3fSimd, 16 B), 3x3 blocks as 9

@@ -53,6 +53,27 @@ __device__ __forceinline__ float4 ld_wt(const float4* p) {
     return make_float4(a.x, a.y, b.x, b.y);
 }
 
+// Left fold of n4 float4 (4 n4 floats, n4 a multiple of B) of one LDS row into
+// acc, in order, B float4 per batch: the batch's B reads issue together and the
+// adds wait for them one by one, so one LDS latency is exposed per 4 B adds
+// (scripts/dev/fold_rate.hip: cycles per add for B = 8 / 16 / 32).
+template <int B = 8>
+__device__ __forceinline__ float fold_row(const float4* __restrict__ row, int n4, float acc) {
+    for (int k0 = 0; k0 < n4; k0 += B) {
+        float4 c[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) c[k] = row[k0 + k];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            acc = __fadd_rn(acc, c[k].x);
+            acc = __fadd_rn(acc, c[k].y);
+            acc = __fadd_rn(acc, c[k].z);
+            acc = __fadd_rn(acc, c[k].w);
+        }
+    }
+    return acc;
+}
+
 constexpr int kDeepChunk = 2048;  // list entries staged per step (8 per thread): one step at 1M
 
 // R3 of node `node` folded from R1 (see the header), published; the block's
@@ -112,28 +133,9 @@ __device__ __forceinline__ void deep_node(const float4* __restrict__ inv, int no
         if (PREFETCH && b0 == 0 && w == 1) load_record<true>(inv, blk, lane, g, tl);
         if (b0 + kDeepChunk < len) load(b0 + kDeepChunk);  // in flight during the fold
         if (t < 3) {
-            // cnt is a multiple of 32 (stride): whole 8-float4 batches, the
-            // next batch's reads in flight behind the current batch's 32 adds
+            // cnt is a multiple of 32 (stride): whole 8-float4 batches
             const int n4 = min(kDeepChunk, len - b0) / 4;
-            const float4* row = reinterpret_cast<const float4*>(st[t]);
-            float4 cur[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = row[k];
-            for (int k0 = 0; k0 < n4; k0 += 8) {
-                const int kn = k0 + 8 < n4 ? k0 + 8 : k0;
-                float4 nxt[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) nxt[k] = row[kn + k];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    acc = __fadd_rn(acc, cur[k].x);
-                    acc = __fadd_rn(acc, cur[k].y);
-                    acc = __fadd_rn(acc, cur[k].z);
-                    acc = __fadd_rn(acc, cur[k].w);
-                }
-#pragma unroll
-                for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
-            }
+            acc = fold_row(reinterpret_cast<const float4*>(st[t]), n4, acc);
         }
     }
     MAS_STAMP(1, pw, 2);

@@ -366,9 +366,14 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     hipEvent_t* ev = nullptr;
     if (h->profiling && h->profRecorded < kProfRing) ev = &h->prof[4 * h->profRecorded++];
     if (ev) hipEventRecord(ev[0], s);
-    // coarse levels (mas_internal.h coarseMode); both forms bitwise equal
-    if (h->L > 2 && h->coarseMode == 3 && coarse1_supported(h)) launch_coarse_one(h, d_r, s);
-    else if (h->L > 2 && h->coarseMode == 2) launch_coarse_twopass(h, d_r, s);
+    // coarse levels (mas_internal.h coarseMode); every form bitwise equal.  The
+    // one-launch form's tags carry a host-side epoch, which a graph capture
+    // would freeze: a capturing stream gets the two-launch form.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (h->L > 2 && h->coarseMode == 3 && hipStreamIsCapturing(s, &cap) == hipSuccess &&
+        cap == hipStreamCaptureStatusNone && coarse1_supported(h))
+        launch_coarse_one(h, d_r, s);
+    else if (h->L > 2 && h->coarseMode >= 2) launch_coarse_twopass(h, d_r, s);
     else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
     if (ev) hipEventRecord(ev[1], s);
     launch_fine(h, 0, h->nFineBlk, d_r, d_z, s, h->applyDone, h->applyRzPart);

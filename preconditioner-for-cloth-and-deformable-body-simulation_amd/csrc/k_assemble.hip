@@ -895,7 +895,27 @@ int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const in
 static int fork_fused(mas_context* h, const FineAsm& fa, hipStream_t s) {
     int rc;
     if (!h->prepStream) {
-        rc = hip_check(h, hipStreamCreateWithFlags(&h->prepStream, hipStreamNonBlocking), "prepare stream");
+        // MAS_PREP_CU_RESERVE=k (A/B): the fused kernel's queue leaves k CUs
+        // to this stream's coarse assembly, which otherwise gets no slot while
+        // the fused kernel's 32 768 waves hold every CU.  The reserved CUs are
+        // spread over the mask so that every XCD loses the same number whether
+        // the bits map to XCDs by bit % 8 or by bit / 32.
+        int reserve = 0;
+        if (const char* e = std::getenv("MAS_PREP_CU_RESERVE")) reserve = std::atoi(e);
+        hipDeviceProp_t prop{};
+        if (reserve > 0 && hipGetDeviceProperties(&prop, h->device) == hipSuccess &&
+            prop.multiProcessorCount % 32 == 0 && reserve % 8 == 0 && reserve <= prop.multiProcessorCount / 2) {
+            const int n = prop.multiProcessorCount, words = n / 32, per = n / 8;
+            std::vector<uint32_t> mask(words, 0xffffffffu);
+            for (int j = 0; j < reserve; ++j) {
+                const int x = j % 8, y = j / 8;
+                const int bit = per * x + (8 * (y % (per / 8)) + x + y / (per / 8)) % per;
+                mask[bit / 32] &= ~(1u << (bit % 32));
+            }
+            rc = hip_check(h, hipExtStreamCreateWithCUMask(&h->prepStream, words, mask.data()), "prepare stream");
+        } else {
+            rc = hip_check(h, hipStreamCreateWithFlags(&h->prepStream, hipStreamNonBlocking), "prepare stream");
+        }
         if (rc || (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepFork, hipEventDisableTiming), "event")) ||
             (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepJoin, hipEventDisableTiming), "event")) ||
             (rc = hip_check(h, hipEventCreate(&h->evFine[0]), "event")) ||

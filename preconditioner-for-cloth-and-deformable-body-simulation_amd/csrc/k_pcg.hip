@@ -439,6 +439,24 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_true_finish(const double* _
 }
 
 // Ap = A p; partials p.Ap
+#ifndef MAS_SPMV_PIPE
+#define MAS_SPMV_PIPE 1
+#endif
+// One ELL row group's matrix stream: the neighbour ids and the nine
+// component rows of its 64 slots (spmv_rows_ell's layout).
+struct EllSlot {
+    int nb;
+    float m[9];
+};
+template <int G>
+__device__ __forceinline__ void ell_load(int g0, int lane, const float* __restrict__ ellOff,
+                                         const int* __restrict__ ellIdx, EllSlot& e) {
+    e.nb = __builtin_nontemporal_load(ellIdx + (size_t)g0 * 64 + lane);
+    __builtin_amdgcn_sched_barrier(0);  // nb first: the gathers wait for it alone
+#pragma unroll
+    for (int q = 0; q < 9; ++q) e.m[q] = __builtin_nontemporal_load(ellOff + (size_t)g0 * 576 + q * 64 + lane);
+}
+
 template <int G>
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __restrict__ starts,
                                                           const int* __restrict__ idx, const float* __restrict__ diag,
@@ -452,15 +470,65 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __r
     constexpr int rowsPerWave = kSpmvRows * (64 / G);
     XcdRows xr(nV, rowsPerWave);
     double pap = 0.0;
-    for (int base = xr.first; base < xr.end; base += xr.stride) {
-        int v[kSpmvRows];
-        float3 y[kSpmvRows];
-        spmv_rows_ell<G, kSpmvRows>(base, nV, lane, starts, idx, diag, off, ellOff, ellIdx, p, v, y);
+    if (MAS_SPMV_PIPE && MAS_SPMV_NT && kSpmvRows == 1) {
+        // Software-pipelined over the wave's passes: the next group's matrix
+        // stream is issued after this group's vector gathers, so it is in
+        // flight while they return and the block products run (the load
+        // counter is in order: loads issued before the gathers would have to
+        // land first).  Same entries, lanes and order as spmv_rows_ell.
+        // Branch-free until the products (clamped addresses; a branch would
+        // make the compiler drain every load at the join).
+        const int lastGroup = (xr.end - 1) / (64 / G);
+        // one pass: cur's products, nxt's stream issued after cur's gathers;
+        // the two buffers alternate (a register copy would wait for the loads)
+        auto pass = [&](int base, const EllSlot& cur, EllSlot& nxt) {
+            const int v = base + lane / G;
+            const bool valid = v < nV;
+            const int vc = valid ? v : 0;
+            const float4 xn = p[cur.nb >= 0 ? cur.nb : 0];
+            const float4 xd = p[vc];
+            const int e = starts[vc] + sub, e1 = valid ? starts[vc + 1] : 0;
+            float dg[9];
+            __builtin_memcpy(dg, diag + 9 * (size_t)vc, 36);
+            ell_load<G>(min((base + xr.stride) / (64 / G), lastGroup), lane, ellOff, ellIdx, nxt);
+            const float3 zero = make_float3(0.f, 0.f, 0.f);
+            const float3 dp = mat3_mul(dg, xd);
+            float3 acc = sub == 0 && valid ? dp : zero;
+            float3 withN = acc;
+            add3(withN, mat3_mul(cur.m, xn));
+            if (cur.nb >= 0) acc = withN;
+            for (int ee = e + G; ee < e1; ee += G) add3(acc, mat3_mul(off + 9 * (size_t)ee, p[idx[ee]]));
 #pragma unroll
-        for (int q = 0; q < kSpmvRows; ++q) {
-            if (sub == 0 && v[q] < nV) {
-                ap[v[q]] = make_float4(y[q].x, y[q].y, y[q].z, 0.f);
-                pap += dot3(y[q], p[v[q]]);
+            for (int o = G / 2; o > 0; o >>= 1) {
+                acc.x = __fadd_rn(acc.x, __shfl_xor(acc.x, o));
+                acc.y = __fadd_rn(acc.y, __shfl_xor(acc.y, o));
+                acc.z = __fadd_rn(acc.z, __shfl_xor(acc.z, o));
+            }
+            if (sub == 0 && valid) {
+                ap[v] = make_float4(acc.x, acc.y, acc.z, 0.f);
+                pap += dot3(acc, xd);
+            }
+        };
+        EllSlot a, b;
+        ell_load<G>(min(xr.first / (64 / G), lastGroup), lane, ellOff, ellIdx, a);
+        for (int base = xr.first; base < xr.end;) {
+            pass(base, a, b);
+            base += xr.stride;
+            if (base >= xr.end) break;
+            pass(base, b, a);
+            base += xr.stride;
+        }
+    } else {
+        for (int base = xr.first; base < xr.end; base += xr.stride) {
+            int v[kSpmvRows];
+            float3 y[kSpmvRows];
+            spmv_rows_ell<G, kSpmvRows>(base, nV, lane, starts, idx, diag, off, ellOff, ellIdx, p, v, y);
+#pragma unroll
+            for (int q = 0; q < kSpmvRows; ++q) {
+                if (sub == 0 && v[q] < nV) {
+                    ap[v[q]] = make_float4(y[q].x, y[q].y, y[q].z, 0.f);
+                    pap += dot3(y[q], p[v[q]]);
+                }
             }
         }
     }

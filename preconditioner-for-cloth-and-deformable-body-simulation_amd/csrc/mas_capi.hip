@@ -151,6 +151,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (h->cfg.reference_formation) h->factorVariant = 4;
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
+    if (const char* v = std::getenv("MAS_C1_L1DELAY")) h->c1L1Delay = std::atoi(v);
     int rc = upload_slot_table(h);
     if (rc != MAS_OK) {
         mas_destroy(h);

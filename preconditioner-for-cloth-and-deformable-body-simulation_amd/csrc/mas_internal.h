@@ -116,12 +116,11 @@ struct mas_context {
     // formation (not bitwise, the default; mas_config.reference_formation = 1
     // selects 4); 0 = LDS-row k_factor
     int factorVariant = 5;
-    // coarse levels (env MAS_COARSE_MODE): 3 = one launch (k_coarse1.hip, L >= 3);
-    // 2 = two launches, restrictions then
-    // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (One-launch
-    // forms and the side-stream overlap were measured slower: DESIGN.md
-    // section 4.)
-    int coarseMode = 2;
+    // coarse levels (env MAS_COARSE_MODE): 3 = one launch with tagged
+    // hand-offs (k_coarse1.hip, L >= 3); 2 = two launches, restrictions then
+    // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (The
+    // side-stream overlap was measured slower: DESIGN.md section 4.)
+    int coarseMode = 3;
     // coarse launches in their occupancy forms (k_coarse.hip): -1 = when the
     // level-1 level has >= kCoarseOccBlocks blocks, 0 = never, 1 = always;
     // env MAS_COARSE_OCC
@@ -169,9 +168,12 @@ struct mas_context {
     // every level-1 node, R1 in list order (deepR1), per-block arrival counters
     mas::Buffer deepKeys, deepVals, deepIdx, deepOff, deepPos, deepR1, deepCnt, deepIdxShard;
     int deepStride = 0;  // list slots per level-3 node (the longest list, rounded up to 4)
-    // one-launch coarse form (k_coarse1.hip): per level-2 block the arrival
-    // counters, then the expected arrival counts (2 x ceil(n2 / 32) ints)
-    mas::Buffer l2Cnt, l1info;
+    // one-launch coarse form (k_coarse1.hip): tagged hand-off slots (level-3
+    // lists, level-2 nodes, level-3 nodes), per level-1 node (parent, mask,
+    // list slot); the apply epoch the tags carry (0 after Prepare)
+    mas::Buffer c1Tags, l1info;
+    unsigned coarse1Epoch = 0;
+    int c1L1Delay = 0;  // A/B (env MAS_C1_L1DELAY): bank waves sleep before the level-1 inverse load
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
     mas::Buffer pcgRzPart;                               // PCG: r.z partials of the fine apply kernel
@@ -222,7 +224,7 @@ struct mas_context {
                               &vlist, &voff, &tab, &termCnt, &termOff, &terms,
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cFineVal, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
-                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &l2Cnt, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart};
         for (mas::Buffer* b : all) f(*b);
     }
@@ -265,7 +267,7 @@ int build_l1src(mas_context* h, hipStream_t s);
 void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s);
 void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s);  // k_coarse1.hip (L >= 3)
 int build_coarse1_tables(mas_context* h, hipStream_t s);
-bool coarse1_supported(const mas_context* h);  // every level-3 list fits a fold wave (k_coarse1.hip)
+bool coarse1_supported(const mas_context* h);  // the tag slots exist (k_coarse1.hip)
 void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
 void launch_coarse_deep(mas_context* h, const float4* src, const int* idx, hipStream_t s);
 int deep_nodes(const mas_context* h);  // level-3 node ids incl. padding (0 below L = 4)

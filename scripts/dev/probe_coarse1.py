@@ -27,20 +27,22 @@ for it in range(20):
     torch.cuda.synchronize()
     P.PreconditioningDevice(z, r, 0)
     torch.cuda.synchronize()
-buf = np.zeros(2 * 8192 * 8, np.uint64)
+buf = np.zeros(3 * 8192 * 8, np.uint64)
 lib.mas_probe1_dump(buf.ctypes.data, buf.size)
-buf = buf.reshape(2, 8192, 8).astype(np.int64)
+buf = buf.reshape(3, 8192, 8).astype(np.int64)
 t0 = buf[buf > 0].min()
 print(name, "levels", P.info()["level_size"].tolist())
-labels = {0: ["start", "-", "fold end", "arrived", "block solved"],
-          1: ["start", "staged", "R1/R2 folded", "stores drained", "arrival known", "Z1 stored", "Z2 solved"]}
-for kind in (0, 1):
+labels = {0: ["start", "first prefix", "fold end", "R3 published"],
+          1: ["start", "staged", "R1/R2 published", "Z1 stored"],
+          2: ["start", "R polled", "Z stored"]}
+names = {0: "level-3 fold waves", 1: "bank waves", 2: "level-2/3 solve waves"}
+for kind in (0, 1, 2):
     b = buf[kind]
     live = b[:, 0] > 0
     if not live.any():
         continue
     b = b[live]
-    print(f"{'level-3 fold waves' if kind == 0 else 'bank waves'}: {len(b)}")
+    print(f"{names[kind]}: {len(b)}")
     for s, lab in enumerate(labels[kind]):
         m = b[:, s] > 0
         if not m.any():
