@@ -112,9 +112,11 @@ __device__ __forceinline__ void contact_h(const DevStencil& s, float (&hm)[9]) {
 }
 
 // counts: dCnt[i] block-entry records, aCnt[i] additional records of stencil i
+// skip0: without the level-0 records (block entries of same-bank pairs, the
+// w^2 additional rows), which run_level0_early built already
 __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restrict__ st, int n,
                                                        const int* __restrict__ gn, int L, int* __restrict__ dCnt,
-                                                       int* __restrict__ aCnt) {
+                                                       int* __restrict__ aCnt, bool skip0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
     if (i == n) {  // closes the exclusive scans
@@ -122,13 +124,13 @@ __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restr
         return;
     }
     const DevStencil s = st[i];
-    int d = 0, a = s.n;
+    int d = 0, a = skip0 ? 0 : s.n;
     for (int x = 0; x < s.n; ++x)
         for (int y = x + 1; y < s.n; ++y) {
             unsigned my = (unsigned)s.idx[x], ot = (unsigned)s.idx[y];
             const int level = climb(gn, L, my, ot);
             if (level >= L) continue;
-            d += 2;
+            if (level > 0 || !skip0) d += 2;
             if (level < L - 1) a += gn[my] == gn[ot] ? 1 : 2;
         }
     dCnt[i] = d;
@@ -143,14 +145,14 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
                                                        const int* __restrict__ dOff, const int* __restrict__ aOff,
                                                        EntryKey* __restrict__ dKeys, int* __restrict__ dIds,
                                                        float* __restrict__ dVal, unsigned* __restrict__ aKeys,
-                                                       int* __restrict__ aIds, float* __restrict__ aVal) {
+                                                       int* __restrict__ aIds, float* __restrict__ aVal, bool skip0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const DevStencil s = st[i];
     float hm[9];
     contact_h(s, hm);
     int d = dOff[i], a = aOff[i];
-    for (int it = 0; it < s.n; ++it, ++a) {  // .cpp:1214-1217: additional[idx] += h w^2
+    for (int it = 0; it < s.n && !skip0; ++it, ++a) {  // .cpp:1214-1217: additional[idx] += h w^2
         const float w2 = __fmul_rn(s.w[it], s.w[it]);
         aKeys[a] = (unsigned)s.idx[it];
         aIds[a] = a;
@@ -164,13 +166,15 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
             const float ww = __fmul_rn(s.w[x], s.w[y]);
             float t[9];
             for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e]);
-            // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot]
-            dKeys[d] = (EntryKey)((my << 5) | (ot & 31u));
-            dKeys[d + 1] = (EntryKey)((ot << 5) | (my & 31u));
-            dIds[d] = d;
-            dIds[d + 1] = d + 1;
-            for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
-            d += 2;
+            if (level > 0 || !skip0) {
+                // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot]
+                dKeys[d] = (EntryKey)((my << 5) | (ot & 31u));
+                dKeys[d + 1] = (EntryKey)((ot << 5) | (my & 31u));
+                dIds[d] = d;
+                dIds[d + 1] = d + 1;
+                for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
+                d += 2;
+            }
             if (level < L - 1) {
                 const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
                 if (pm == po) {
@@ -187,6 +191,60 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
                     a += 2;
                 }
             }
+        }
+}
+
+// Level-0 records alone (run_level0_early): per stencil the block-entry
+// records of its same-bank pairs (level 0 of k_contact_write's loop: same
+// order, same values) at dOff[i], and its w^2 additional records at the fixed
+// slots kA0 i + it (slots past s.n keep the sentinel key).  No level ids are
+// needed: a pair is a level-0 entry iff both vertices share a level-0 bank.
+constexpr int kA0 = 5;  // most vertices per stencil (EF)
+__global__ __launch_bounds__(256) void k_contact0_count(const DevStencil* __restrict__ st, int n, int* __restrict__ dCnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {
+        dCnt[n] = 0;
+        return;
+    }
+    const DevStencil s = st[i];
+    int d = 0;
+    for (int x = 0; x < s.n; ++x)
+        for (int y = x + 1; y < s.n; ++y) d += ((unsigned)s.idx[x] >> 5) == ((unsigned)s.idx[y] >> 5) ? 2 : 0;
+    dCnt[i] = d;
+}
+
+__global__ __launch_bounds__(256) void k_contact0_write(const DevStencil* __restrict__ st, int n,
+                                                        const int* __restrict__ dOff, EntryKey* __restrict__ dKeys,
+                                                        int* __restrict__ dIds, float* __restrict__ dVal,
+                                                        unsigned* __restrict__ aKeys, int* __restrict__ aIds,
+                                                        float* __restrict__ aVal) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const DevStencil s = st[i];
+    float hm[9];
+    contact_h(s, hm);
+    for (int it = 0; it < s.n; ++it) {  // .cpp:1214-1217: additional[idx] += h w^2
+        const int a = kA0 * i + it;
+        const float w2 = __fmul_rn(s.w[it], s.w[it]);
+        aKeys[a] = (unsigned)s.idx[it];
+        aIds[a] = a;
+        for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = __fmul_rn(hm[e], w2);
+    }
+    int d = dOff[i];
+    for (int x = 0; x < s.n; ++x)
+        for (int y = x + 1; y < s.n; ++y) {
+            const unsigned my = (unsigned)s.idx[x], ot = (unsigned)s.idx[y];
+            if ((my >> 5) != (ot >> 5)) continue;
+            const float ww = __fmul_rn(s.w[x], s.w[y]);
+            float t[9];
+            for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e]);
+            dKeys[d] = (EntryKey)((my << 5) | (ot & 31u));
+            dKeys[d + 1] = (EntryKey)((ot << 5) | (my & 31u));
+            dIds[d] = d;
+            dIds[d + 1] = d + 1;
+            for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
+            d += 2;
         }
 }
 
@@ -892,16 +950,16 @@ int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const in
 // and the prefolded level-0 contact entries); run_factor joins
 // (measured: a CU-masked side stream, stream priorities and a persistent
 // fused grid all lost to this plain form).
-static int fork_fused(mas_context* h, const FineAsm& fa, hipStream_t s) {
-    int rc;
+int prep_stream_init(mas_context* h) {
+    int rc = MAS_OK;
     if (!h->prepStream) {
-        // MAS_PREP_CU_RESERVE=k (A/B): the fused kernel's queue leaves k CUs
-        // to this stream's coarse assembly, which otherwise gets no slot while
-        // the fused kernel's 32 768 waves hold every CU.  The reserved CUs are
+        // The fused kernel's queue leaves prepCuReserve CUs (env
+        // MAS_PREP_CU_RESERVE) to the caller's stream: without that the coarse
+        // assembly gets no slot while the fused kernel's 32 768 waves hold
+        // every CU, and the two run one after the other.  The reserved CUs are
         // spread over the mask so that every XCD loses the same number whether
         // the bits map to XCDs by bit % 8 or by bit / 32.
-        int reserve = 0;
-        if (const char* e = std::getenv("MAS_PREP_CU_RESERVE")) reserve = std::atoi(e);
+        const int reserve = h->prepCuReserve;
         hipDeviceProp_t prop{};
         if (reserve > 0 && hipGetDeviceProperties(&prop, h->device) == hipSuccess &&
             prop.multiProcessorCount % 32 == 0 && reserve % 8 == 0 && reserve <= prop.multiProcessorCount / 2) {
@@ -919,9 +977,16 @@ static int fork_fused(mas_context* h, const FineAsm& fa, hipStream_t s) {
         if (rc || (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepFork, hipEventDisableTiming), "event")) ||
             (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepJoin, hipEventDisableTiming), "event")) ||
             (rc = hip_check(h, hipEventCreate(&h->evFine[0]), "event")) ||
-            (rc = hip_check(h, hipEventCreate(&h->evFine[1]), "event")))
+            (rc = hip_check(h, hipEventCreate(&h->evFine[1]), "event")) ||
+            (rc = hip_check(h, hipEventCreateWithFlags(&h->evAdd0, hipEventDisableTiming), "event")))
             return rc;
     }
+    return rc;
+}
+
+static int fork_fused(mas_context* h, const FineAsm& fa, hipStream_t s) {
+    int rc;
+    if ((rc = prep_stream_init(h))) return rc;
     // MAS_PREP_SERIAL=1 (A/B): the same kernel in line on the caller's stream
     static const bool serial = std::getenv("MAS_PREP_SERIAL") && std::atoi(std::getenv("MAS_PREP_SERIAL"));
     hipStream_t ps = serial ? s : h->prepStream;
@@ -948,9 +1013,10 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     if (B + RecKey::kLaneBits > 32) return fail(h, MAS_ERR_ARG, "contact entry keys: more than 2^27 nodes");
     if ((rc = ensure(h, h->cdCnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->cdOff, (size_t)(n + 1) * 4)) ||
         (rc = ensure(h, h->caCnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->caOff, (size_t)(n + 1) * 4)) ||
-        (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4)))
+        (!h->earlyFused && (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4))))  // prepStream's otherwise
         return rc;
-    k_contact_count<<<cdiv(n + 1, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdCnt), P<int>(h->caCnt));
+    const bool skip0 = h->earlyFused;  // level-0 records built by run_level0_early
+    k_contact_count<<<cdiv(n + 1, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdCnt), P<int>(h->caCnt), skip0);
     if ((rc = exclusive_scan(h, P<int>(h->cdCnt), P<int>(h->cdOff), n + 1, s, "contact scan")) ||
         (rc = exclusive_scan(h, P<int>(h->caCnt), P<int>(h->caOff), n + 1, s, "contact scan")))
         return rc;
@@ -968,7 +1034,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdOff), P<int>(h->caOff),
                                                  P<EntryKey>(h->cdKeys), P<int>(h->cdIds),
                                                  P<float>(h->cdVal), P<unsigned>(h->caKeys), P<int>(h->caIds),
-                                                 P<float>(h->caVal));
+                                                 P<float>(h->caVal), skip0);
     if ((rc = sort_pairs(h, P<EntryKey>(h->cdKeys), P<EntryKey>(h->cdKeysS), P<int>(h->cdIds),
                          P<int>(h->cdIdsS), nD, B + RecKey::kLaneBits, s, "contact entry sort")) ||
         (rc = sort_pairs(h, P<unsigned>(h->caKeys), P<unsigned>(h->caKeysS), P<int>(h->caIds), P<int>(h->caIdsS), nA,
@@ -976,7 +1042,8 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         return rc;
     float* dense = dense_base(h);
     // fine entries: k_level0_block; coarse entries: folded onto the zeroed coarse blocks
-    k_contact_fine_bounds<<<cdiv(nD + 1, 256), 256, 0, s>>>(nD, RecKey::kLaneBits, begin1, h->nFineBlk,
+    if (!skip0)
+        k_contact_fine_bounds<<<cdiv(nD + 1, 256), 256, 0, s>>>(nD, RecKey::kLaneBits, begin1, h->nFineBlk,
                                                             P<EntryKey>(h->cdKeysS), P<int>(h->cFineOff));
     // additional rows (level 0 and coarse), folded from zero
     if (nA > 0)
@@ -985,7 +1052,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
             NodeRow{P<float>(h->additional)});
     fc = FineContacts{P<EntryKey>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
                       RecKey::kLaneBits};
-    if (h->factorVariant >= 4) {
+    if (h->factorVariant >= 4 && !skip0) {
         if (nD > 0) {
             // each level-0 entry's contact run folded from zero once (the fused
             // kernel adds it to its zero entry)
@@ -1005,8 +1072,12 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     }
     k_push_count<<<cdiv(nA + 1, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), gn, P<int>(h->cpCnt));
     if ((rc = exclusive_scan(h, P<int>(h->cpCnt), P<int>(h->cpOff), nA + 1, s, "push scan"))) return rc;
-    int pf[2] = {0, 0};  // push count, first coarse block-entry record
-    if ((rc = read_back(h, s, {P<int>(h->cpOff) + nA, P<int>(h->cFineOff) + h->nFineBlk}, pf))) return rc;
+    int pf[2] = {0, 0};  // push count, first coarse block-entry record (0: no level-0 records here)
+    if (skip0) {
+        if ((rc = read_back(h, s, {P<int>(h->cpOff) + nA}, pf))) return rc;
+    } else if ((rc = read_back(h, s, {P<int>(h->cpOff) + nA, P<int>(h->cFineOff) + h->nFineBlk}, pf))) {
+        return rc;
+    }
     const int nP = pf[0], fineEnd = pf[1];
     const RecKey rk{0, B};
     if (nD > fineEnd)
@@ -1029,6 +1100,135 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     return hip_check(h, hipGetLastError(), "contact kernels");
 }
 
+// The level-0 blocks need only level-0 data -- the sorted vertices' CSR rows,
+// the level-0 contact entries and additional rows -- not the coarse levels.
+// So right after the stencils the caller's stream forks prepStream, which
+// builds the level-0 contact records (k_contact0_*: no level ids, no host
+// read: sizes are bounded by the stencil count and the tails carry the
+// sentinel key), sorts and folds them exactly as run_contacts does for rows
+// < begin_1, and starts the fused assemble + factor kernel, while the caller's
+// stream builds the levels, the coarse contact records (run_contacts skips the
+// level-0 ones) and the coarse assembly on the CUs the fused kernel's queue
+// leaves free (prep_stream_init).  Same records in the same order: every
+// block bitwise as before.
+// od and the coarse record counts (k_od / k_od_lanes): level-0 data only.
+// Lanes per vertex: the largest neighbour count (ELL slot 0 is the vertex
+// itself), a power of two.
+static void launch_od(mas_context* h, const FineAsm& fa, hipStream_t s) {
+    const int nV = h->nV, val = h->maxNbr - 1;
+    if (val <= 8) k_od_lanes<8><<<cdiv((long long)nV * 8, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+    else if (val <= 16) k_od_lanes<16><<<cdiv((long long)nV * 16, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+    else if (val <= 32) k_od_lanes<32><<<cdiv((long long)nV * 32, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+    else k_od<<<cdiv(nV, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+}
+
+bool early_fused_wanted(const mas_context* h) {
+    const int nv32 = h->nFineBlk * 32;
+    return h->factorVariant >= 4 && !h->cfg.keep_blocks && nv32 > 0 &&
+           bit_width((unsigned)(nv32 - 1)) + 1 + RecKey::kLaneBits <= 32;  // level-0 keys fit (else the late path)
+}
+
+int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s) {
+    h->earlyFused = false;
+    if (!early_fused_wanted(h)) return MAS_OK;
+    int rc;
+    if ((rc = prep_stream_init(h))) return rc;
+    static const bool serial = std::getenv("MAS_PREP_SERIAL") && std::atoi(std::getenv("MAS_PREP_SERIAL"));
+    hipStream_t ps = serial ? s : h->prepStream;
+    const int nV = h->nV, n = h->nStencil, nv32 = h->nFineBlk * 32;
+    // the level-0 inverses go straight into inv: room for them now, and for a
+    // coarse share like the previous Prepare's (run_assemble grows it keeping
+    // the level-0 part if the hierarchy needs more)
+    const size_t blockBytes = (size_t)kBlockFloats * 4;
+    const size_t want = (size_t)std::max(h->nBlk, h->nFineBlk + h->nFineBlk / 8 + 64) * blockBytes;
+    if (h->inv.bytes < (size_t)h->nFineBlk * blockBytes && (rc = ensure(h, h->inv, want))) return rc;
+    if ((rc = ensure(h, h->add0, (size_t)nv32 * 36))) return rc;
+    // evPrepFork was recorded on s right after the stencils (run_prepare), before
+    // the level kernels: prepStream waits for the stencils only
+    if ((rc = hip_check(h, hipStreamWaitEvent(ps, h->evPrepFork, 0), "fork wait")) ||
+        (rc = hip_check(h, hipMemsetAsync(h->add0.p, 0, (size_t)nv32 * 36, ps), "memset add0")))
+        return rc;
+    FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges,
+               P<float>(h->add0), nullptr, nullptr, nullptr, 0, nullptr};
+    if (n > 0) {
+        const size_t ubD = (size_t)n * kA0 * (kA0 - 1), ubA = (size_t)n * kA0;  // 2 C(5, 2) entries, 5 rows per stencil
+        if (ubD > 0x7fffffff) return fail(h, MAS_ERR_ARG, "too many contact stencils");
+        if ((rc = ensure(h, h->c0Cnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->c0Off, (size_t)(n + 1) * 4)) ||
+            (rc = ensure(h, h->c0Keys, ubD * 4)) || (rc = ensure(h, h->c0KeysS, ubD * 4)) ||
+            (rc = ensure(h, h->c0Ids, ubD * 4)) || (rc = ensure(h, h->c0IdsS, ubD * 4)) ||
+            (rc = ensure(h, h->c0Val, ubD * 36)) || (rc = ensure(h, h->a0Keys, ubA * 4)) ||
+            (rc = ensure(h, h->a0KeysS, ubA * 4)) || (rc = ensure(h, h->a0Ids, ubA * 4)) ||
+            (rc = ensure(h, h->a0IdsS, ubA * 4)) || (rc = ensure(h, h->a0Val, ubA * 36)) ||
+            (rc = ensure(h, h->cFineVal, ubD * 36)) || (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4)))
+            return rc;
+        // sentinel keys past the records; their ids index record 0 (never
+        // folded: a sentinel is dead, but no index is left undefined)
+        if ((rc = hip_check(h, hipMemsetAsync(h->c0Keys.p, 0xff, ubD * 4, ps), "memset keys")) ||
+            (rc = hip_check(h, hipMemsetAsync(h->a0Keys.p, 0xff, ubA * 4, ps), "memset keys")) ||
+            (rc = hip_check(h, hipMemsetAsync(h->c0Ids.p, 0, ubD * 4, ps), "memset ids")) ||
+            (rc = hip_check(h, hipMemsetAsync(h->a0Ids.p, 0, ubA * 4, ps), "memset ids")))
+            return rc;
+        const DevStencil* st = P<DevStencil>(h->stencils);
+        k_contact0_count<<<cdiv(n + 1, 256), 256, 0, ps>>>(st, n, P<int>(h->c0Cnt));
+        // prepStream's own sort / scan scratch (rs_*(..., side = true)), whatever MAS_SORT selects
+        if ((rc = rs_exclusive_scan(h, P<int>(h->c0Cnt), P<int>(h->c0Off), n + 1, ps, "level-0 contact scan", true)))
+            return rc;
+        k_contact0_write<<<cdiv(n, 256), 256, 0, ps>>>(st, n, P<int>(h->c0Off), P<EntryKey>(h->c0Keys),
+                                                       P<int>(h->c0Ids), P<float>(h->c0Val), P<unsigned>(h->a0Keys),
+                                                       P<int>(h->a0Ids), P<float>(h->a0Val));
+        // one bit above the largest real key: the sentinel (all ones) sorts
+        // after every real key instead of tying with one (the row sentinels
+        // sit between real records, and a tie would split a run)
+        const int vb = std::max(1, bit_width((unsigned)(nv32 - 1))) + 1;
+        if ((rc = rs_sort_pairs(h, P<EntryKey>(h->c0Keys), P<EntryKey>(h->c0KeysS), P<int>(h->c0Ids),
+                                P<int>(h->c0IdsS), (int)ubD, vb + RecKey::kLaneBits, ps, "level-0 contact entry sort",
+                                true)) ||
+            (rc = rs_sort_pairs(h, P<unsigned>(h->a0Keys), P<unsigned>(h->a0KeysS), P<int>(h->a0Ids),
+                                P<int>(h->a0IdsS), (int)ubA, vb, ps, "level-0 contact row sort", true)))
+            return rc;
+        k_contact_fine_bounds<<<cdiv(ubD + 1, 256), 256, 0, ps>>>((int)ubD, RecKey::kLaneBits, nv32, h->nFineBlk,
+                                                                 P<EntryKey>(h->c0KeysS), P<int>(h->cFineOff));
+        k_fold_runs<NodeRow, true, unsigned><<<cdiv(ubA, 64), 64, 0, ps>>>(
+            (int)ubA, 0xffffffffu, P<unsigned>(h->a0KeysS), P<int>(h->a0IdsS), P<float>(h->a0Val),
+            NodeRow{P<float>(h->add0)});
+        k_fold_runs<RunSlot, true, EntryKey><<<cdiv(ubD, 64), 64, 0, ps>>>(
+            (int)ubD, ~0u, P<EntryKey>(h->c0KeysS), P<int>(h->c0IdsS), P<float>(h->c0Val),
+            RunSlot{P<float>(h->cFineVal), (unsigned)nv32});
+        fa.ckeys = P<EntryKey>(h->c0KeysS);
+        fa.cval = P<float>(h->cFineVal);
+        fa.coff = P<int>(h->cFineOff);
+        fa.B = RecKey::kLaneBits;
+    }
+    // od and the record counts need only level-0 data too: computed here on the
+    // whole chip while the levels build, instead of on the caller's reserved CUs
+    if ((rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
+        (rc = hip_check(h, hipMemsetAsync(P<int>(h->recCnt) + nV, 0, 4, ps), "memset recCnt")))
+        return rc;
+    launch_od(h, fa, ps);
+    if ((rc = hip_check(h, hipEventRecord(h->evAdd0, ps), "od ready"))) return rc;
+    h->earlyFused = true;
+    h->earlyFa = fa;
+    return h->fusedAfterLevels ? MAS_OK : launch_level0_fused(h, nullptr);
+}
+
+// the fused kernel on prepStream; s (not null): after everything s has queued
+// (the level build, MAS_FUSED_AFTER_LEVELS)
+int launch_level0_fused(mas_context* h, hipStream_t s) {
+    static const bool serial = std::getenv("MAS_PREP_SERIAL") && std::atoi(std::getenv("MAS_PREP_SERIAL"));
+    int rc;
+    hipStream_t ps = serial && s ? s : h->prepStream;
+    if (s && ps != s &&
+        ((rc = hip_check(h, hipEventRecord(h->evPrepFork, s), "fork")) ||
+         (rc = hip_check(h, hipStreamWaitEvent(ps, h->evPrepFork, 0), "fork wait"))))
+        return rc;
+    if ((rc = hip_check(h, hipEventRecord(h->evFine[0], ps), "record")) ||
+        (rc = launch_factor_fused(h, h->earlyFa, h->fineBlk0, h->fineBlk1, ps)) ||
+        (rc = hip_check(h, hipEventRecord(h->evFine[1], ps), "record")) ||
+        (rc = hip_check(h, hipEventRecord(h->evPrepJoin, ps), "join")))
+        return rc;
+    return MAS_OK;
+}
+
 int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s) {
     const int nV = h->nV, L = h->L, tc = h->totalClusters;
     int rc;
@@ -1037,6 +1237,22 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     h->denseFine = !fused || h->cfg.keep_blocks;
     const int nStored = h->denseFine ? h->nBlk : h->nBlk - h->nFineBlk;
     const size_t denseBytes = (size_t)std::max(nStored, 1) * kDenseFloats * 4;
+    if (h->earlyFused && h->inv.bytes < (size_t)h->nBlk * kBlockFloats * 4) {
+        // the fused kernel is writing the level-0 inverses into inv: let it
+        // finish, then grow inv keeping them (first Prepare of a hierarchy
+        // with more coarse blocks than run_level0_early reserved)
+        Buffer grown;
+        if ((rc = hip_check(h, hipStreamSynchronize(h->prepStream), "prepare stream")) ||
+            (rc = hip_check(h, hipMalloc(&grown.p, (size_t)h->nBlk * kBlockFloats * 4), "hipMalloc inv")))
+            return rc;
+        grown.bytes = (size_t)h->nBlk * kBlockFloats * 4;
+        if ((rc = hip_check(h, hipMemcpyAsync(grown.p, h->inv.p, (size_t)h->nFineBlk * kBlockFloats * 4,
+                                              hipMemcpyDeviceToDevice, s), "keep level-0 inverses")) ||
+            (rc = hip_check(h, hipStreamSynchronize(s), "grow inv")))
+            return rc;
+        hipFree(h->inv.p);
+        h->inv = grown;
+    }
     if ((rc = ensure(h, h->dense, denseBytes)) || (rc = ensure(h, h->inv, (size_t)h->nBlk * kBlockFloats * 4)) ||
         (rc = ensure(h, h->additional, (size_t)(tc + 1) * 36)) ||
         (rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
@@ -1049,27 +1265,28 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
          (rc = hip_check(h, hipMemsetAsync(static_cast<char*>(h->dense.p) + zeroFrom, 0, coarseBytes, s),
                          "memset dense"))) ||
         (rc = hip_check(h, hipMemsetAsync(h->additional.p, 0, (size_t)(tc + 1) * 36, s), "memset additional")) ||
-        (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt")))
+        (!h->earlyFused && (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt"))))
         return rc;
     float* dense = dense_base(h);
     float* add = P<float>(h->additional);
     const int* gn = P<int>(h->goingNext);
     FineContacts fc{};
-    FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges, add,
-               nullptr, nullptr, nullptr, 0, h->cfg.keep_blocks ? dense : nullptr};
+    // level-0 additional rows: add0 when run_level0_early built them
+    FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges,
+               h->earlyFused ? P<float>(h->add0) : add, nullptr, nullptr, nullptr, 0,
+               h->cfg.keep_blocks ? dense : nullptr};
     bool forked = false;
     if (h->nStencil && (rc = run_contacts(h, s, fc, fa, forked))) return rc;
     if (fused) {
         // the level-0 blocks assemble and factor on prepStream while this
         // stream assembles the coarse levels (run_factor joins)
-        if (!forked && (rc = fork_fused(h, fa, s))) return rc;
-        // od and the coarse record counts; lanes per vertex: the largest
-        // neighbour count (ELL slot 0 is the vertex itself), a power of two
-        const int val = h->maxNbr - 1;
-        if (val <= 8) k_od_lanes<8><<<cdiv((long long)nV * 8, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
-        else if (val <= 16) k_od_lanes<16><<<cdiv((long long)nV * 16, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
-        else if (val <= 32) k_od_lanes<32><<<cdiv((long long)nV * 32, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
-        else k_od<<<cdiv(nV, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+        if (h->earlyFused) {
+            // od and the record counts came with the early path (run_level0_early)
+            if ((rc = hip_check(h, hipStreamWaitEvent(s, h->evAdd0, 0), "wait od"))) return rc;
+        } else {
+            if (!forked && (rc = fork_fused(h, fa, s))) return rc;
+            launch_od(h, fa, s);
+        }
     } else {
         k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
                                                   d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt),

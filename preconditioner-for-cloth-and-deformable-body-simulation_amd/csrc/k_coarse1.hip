@@ -103,6 +103,7 @@ struct Coarse1Args {
     unsigned epoch;       // this apply's tag
     int nb1;
     int l1Delay;          // bank waves: s_sleep(32) rounds before the level-1 inverse load (A/B)
+    int pollDelay;        // fold / solve waves: s_sleep(64) rounds before the first poll (A/B)
     const int* done;      // PCG: exit at once when set
 };
 
@@ -213,6 +214,7 @@ __device__ __forceinline__ void fold_wave(const Coarse1Args& a, int T, C1Shared&
     __builtin_amdgcn_s_setprio(3);  // the fold is the launch's longest chain
     float acc = 0.f;  // lanes 0..2: x, y, z
     int e = 0, idle = 0;
+    for (int d = 0; d < a.pollDelay; ++d) __builtin_amdgcn_s_sleep(64);  // nothing is published yet
     if (len > 0) poll(0);
     while (e < len) {
         // the valid prefix of this step's entries (list order = 64 q + lane)
@@ -272,6 +274,7 @@ __device__ __forceinline__ void solve_wave(const Coarse1Args& a, int blk, int lv
     const bool real = lane < 32 && loc < cnt;
     unsigned long long v[3] = {0ull, 0ull, 0ull};
     bool ok = !real;
+    for (int d = 0; d < a.pollDelay; ++d) __builtin_amdgcn_s_sleep(64);
     for (int polls = 0; polls <= kPollLimit; ++polls) {
         if (!ok) {
             ld_tag(tR + loc, v);
@@ -370,6 +373,7 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.tR3 = a.tR2 + ceil32(a.n2);
     a.epoch = h->coarse1Epoch;
     a.l1Delay = h->c1L1Delay;
+    a.pollDelay = h->c1PollDelay;
     a.done = h->applyDone;
     k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3, 64, 0, s>>>(a);
 }

@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <functional>
+
 #include "mas_internal.h"
 
 namespace mas {
@@ -355,7 +357,7 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
 }
 
 // ReorderRealtime, .cpp:415-445
-int run_levels(mas_context* h, hipStream_t s) {
+int run_levels(mas_context* h, hipStream_t s, const std::function<int()>& beforeRead) {
     const int nV = h->nV, L = h->L, nv32 = ceil32(nV);
     const int nB0 = nv32 / 32;
     int rc;
@@ -402,6 +404,8 @@ int run_levels(mas_context* h, hipStream_t s) {
         k_next_level<<<g, 256, 0, s>>>(nV, prev, next, cst + (size_t)level * nV);
     }
     int totals[kMaxLevels + 2] = {};
+    // the host's other work (run_level0_early's launches) while the levels build
+    if (beforeRead && (rc = beforeRead())) return rc;
     if ((rc = read_back(h, s, {tot, tot + 1, tot + 2, tot + 3, tot + 4, tot + 5}, totals))) return rc;
     h->levelSize[2] = totals[1];
     h->levelSize[3] = nv32;

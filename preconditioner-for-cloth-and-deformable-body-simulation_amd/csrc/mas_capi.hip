@@ -152,6 +152,10 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_L1DELAY")) h->c1L1Delay = std::atoi(v);
+    if (const char* v = std::getenv("MAS_C1_POLL_DELAY")) h->c1PollDelay = std::atoi(v);
+    if (const char* v = std::getenv("MAS_PREP_CU_RESERVE")) h->prepCuReserve = std::atoi(v);
+    if (const char* v = std::getenv("MAS_FUSED_AFTER_LEVELS")) h->fusedAfterLevels = std::atoi(v);
+    if (const char* v = std::getenv("MAS_EARLY_THREAD")) h->earlyThread = std::atoi(v);
     int rc = upload_slot_table(h);
     if (rc != MAS_OK) {
         mas_destroy(h);
@@ -176,6 +180,7 @@ int mas_destroy(mas_handle h) {
     }
     if (h->evPrepFork) hipEventDestroy(h->evPrepFork);
     if (h->evPrepJoin) hipEventDestroy(h->evPrepJoin);
+    if (h->evAdd0) hipEventDestroy(h->evAdd0);
     for (auto& e : h->evFine)
         if (e) hipEventDestroy(e);
     release_comm(h);  // drained above; the communicator goes before the buffers it wrote

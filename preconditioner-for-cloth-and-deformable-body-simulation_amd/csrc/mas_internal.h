@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <initializer_list>
 #include <string>
 #include <vector>
@@ -156,6 +157,17 @@ struct mas_context {
     hipStream_t prepStream = nullptr;  // fused level-0 assemble + factor, beside the coarse assembly
     hipEvent_t evPrepFork = nullptr, evPrepJoin = nullptr;
     hipEvent_t evFine[2] = {nullptr, nullptr};  // timing of the fused level-0 kernel (prepare_fine_ms)
+    // early level-0 path (run_level0_early, fused variants): the level-0
+    // contact records and additional rows are built on prepStream right after
+    // the stencils and the fused kernel starts there, beside the level build;
+    // add0 = level-0 additional rows, evAdd0 = they are ready (k_od waits)
+    bool earlyFused = false;
+    int prepCuReserve = 64;  // CUs the fused kernel's queue leaves to the caller's stream (env MAS_PREP_CU_RESERVE)
+    int fusedAfterLevels = 0;  // A/B (env MAS_FUSED_AFTER_LEVELS): the early fused kernel waits for the level build
+    int earlyThread = 1;       // the early path queued from a second host thread (env MAS_EARLY_THREAD)
+    mas::FineAsm earlyFa{};    // its inputs, kept for launch_level0_fused
+    hipEvent_t evAdd0 = nullptr;
+    mas::Buffer add0, c0Cnt, c0Off, c0Keys, c0KeysS, c0Ids, c0IdsS, c0Val, a0Keys, a0KeysS, a0Ids, a0IdsS, a0Val;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
     // contact records (k_assemble.hip): block entries (d*), additional rows (a*), pushes (p*)
@@ -174,6 +186,7 @@ struct mas_context {
     mas::Buffer c1Tags, l1info;
     unsigned coarse1Epoch = 0;
     int c1L1Delay = 0;  // A/B (env MAS_C1_L1DELAY): bank waves sleep before the level-1 inverse load
+    int c1PollDelay = 0;  // A/B (env MAS_C1_POLL_DELAY): fold / solve waves sleep before their first poll
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
     mas::Buffer pcgRzPart;                               // PCG: r.z partials of the fine apply kernel
@@ -206,6 +219,10 @@ struct mas_context {
     // look-back-free radix sort and scan (rsort.hip): ping-pong keys/values,
     // per-tile digit counts, scan tile sums; env MAS_SORT=0 selects rocprim (A/B)
     mas::Buffer rsKeys, rsVals, rsHist, rsPart;
+    // the same scratch for work queued on prepStream (run_level0_early), which
+    // runs beside the caller's stream: sharing one set raced and a regrowth
+    // freed a buffer the other stream was still reading
+    mas::Buffer rsKeysP, rsValsP, rsHistP, rsPartP;
     int sortImpl = 1;
     // events: [0..1] allocate, [2..3] prepare
     hipEvent_t ev[4] = {};
@@ -225,7 +242,8 @@ struct mas_context {
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cFineVal, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
                               &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
-                              &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart};
+                              &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart, &rsKeysP, &rsValsP, &rsHistP, &rsPartP, &add0, &c0Cnt, &c0Off, &c0Keys, &c0KeysS, &c0Ids, &c0IdsS,
+                              &c0Val, &a0Keys, &a0KeysS, &a0Ids, &a0IdsS, &a0Val};
         for (mas::Buffer* b : all) f(*b);
     }
 };
@@ -255,8 +273,16 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
                 hipStream_t s);
 int build_stencils(mas_context* h, const void* ef, const void* ee, const void* vf, const unsigned* efC,
                    const unsigned* eeC, const unsigned* vfC, hipStream_t s);
-int run_levels(mas_context* h, hipStream_t s);
+// beforeRead: called after the level kernels are queued, before the one host read
+int run_levels(mas_context* h, hipStream_t s, const std::function<int()>& beforeRead = {});
 int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s);
+// the level-0 contact path and the fused level-0 kernel on prepStream, right
+// after the stencils (fused variants without keep_blocks); sets earlyFused
+int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s);
+// the early fused kernel itself, when it waits for the level build (fusedAfterLevels)
+int launch_level0_fused(mas_context* h, hipStream_t s);
+bool early_fused_wanted(const mas_context* h);
+int prep_stream_init(mas_context* h);  // prepStream (CU-masked) and its events
 int run_factor(mas_context* h, hipStream_t s);
 // fused level-0 assemble + factor of blocks [blk0, blk1) (k_factor.hip)
 int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s);
@@ -275,9 +301,11 @@ mas::DeepArgs deep_args(mas_context* h, const float4* src, const int* idx);
 int build_deep_lists(mas_context* h, hipStream_t s);
 int build_deep_shard_idx(mas_context* h, hipStream_t s);
 // rsort.hip: stable sort by the low `bits` key bits; exclusive scan
+// side = true: prepStream's scratch (rsKeysP ...), for work beside the caller's stream
 int rs_sort_pairs(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
-                  hipStream_t s, const char* what);
-int rs_exclusive_scan(mas_context* h, const int* in, int* out, int n, hipStream_t s, const char* what);
+                  hipStream_t s, const char* what, bool side = false);
+int rs_exclusive_scan(mas_context* h, const int* in, int* out, int n, hipStream_t s, const char* what,
+                      bool side = false);
 int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
                    hipStream_t s, const char* what);
 // level-0 blocks [blk0, blkEnd) + prolongation; done / rzPart: PCG hooks (k_apply.hip)

@@ -1,5 +1,7 @@
 // prepare.hip -- PreparePreconditioner orchestration (.cpp:67-98):
 // stencils -> aggregation levels -> block assembly -> batched factor -> apply tables.
+#include <thread>
+
 #include "mas_internal.h"
 
 namespace mas {
@@ -22,11 +24,35 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     ScopedEvents ev;
     if (!ev.ok()) return fail(h, MAS_ERR_HIP, "hipEventCreate");
     hipEvent_t e0 = ev.e[0], e1 = ev.e[1];
-    if ((rc = run_levels(h, s))) return rc;
     // the level-0 blocks this Prepare assembles and factors: all, or those of
-    // the Morton shard set by mas_set_prepare_shard (mas_shard_plan's split)
+    // the Morton shard set by mas_set_prepare_shard (mas_shard_plan's split);
+    // level 0 is the sorted vertices, known before the levels are built
+    h->nFineBlk = ceil32(h->nV) / 32;
     h->fineBlk0 = (int)((long long)h->prepRank * h->nFineBlk / h->prepWorld);
     h->fineBlk1 = (int)((long long)(h->prepRank + 1) * h->nFineBlk / h->prepWorld);
+    // fused variants: the level-0 contacts and the fused kernel start on
+    // prepStream after the stencils (the fork event), beside the level build;
+    // their launches are queued while the level kernels run (run_levels' hook)
+    h->earlyFused = false;
+    const bool early = early_fused_wanted(h);
+    if (early && ((rc = prep_stream_init(h)) || (rc = hip_check(h, hipEventRecord(h->evPrepFork, s), "fork"))))
+        return rc;
+    if (early && h->earlyThread) {
+        // a second host thread queues prepStream's work while this one queues
+        // the level build: each stream is fed from the start (one thread
+        // queueing both left the early path behind the level kernels)
+        int earlyRc = MAS_OK;
+        std::thread t([&]() { earlyRc = run_level0_early(h, d_diag9, d_off9, d_ranges, s); });
+        rc = run_levels(h, s);
+        t.join();
+        if (rc) return rc;
+        if (earlyRc) return earlyRc;
+    } else if ((rc = run_levels(h, s, [&]() {
+                    return early ? run_level0_early(h, d_diag9, d_off9, d_ranges, s) : MAS_OK;
+                }))) {
+        return rc;
+    }
+    if (h->earlyFused && h->fusedAfterLevels && (rc = launch_level0_fused(h, s))) return rc;
     hipEventRecord(e0, s);
     if ((rc = run_assemble(h, d_diag9, d_off9, d_ranges, s))) return rc;
     hipEventRecord(e1, s);

@@ -263,7 +263,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(const int* in, int* 
 }  // namespace
 
 int rs_sort_pairs(mas_context* h, const unsigned* kin, unsigned* kout, const int* vin, int* vout, int n, int bits,
-                  hipStream_t s, const char* what) {
+                  hipStream_t s, const char* what, bool side) {
+    Buffer& sKeys = side ? h->rsKeysP : h->rsKeys;
+    Buffer& sVals = side ? h->rsValsP : h->rsVals;
+    Buffer& sHist = side ? h->rsHistP : h->rsHist;
     if (n <= 0) return MAS_OK;
     if (bits <= 0) {  // no key bits: the input order
         int rc = hip_check(h, hipMemcpyAsync(kout, kin, (size_t)n * 4, hipMemcpyDeviceToDevice, s), what);
@@ -273,10 +276,10 @@ int rs_sort_pairs(mas_context* h, const unsigned* kin, unsigned* kout, const int
     const int passes = (bits + 7) / 8, per = (bits + passes - 1) / passes;
     const int nTiles = (int)(((long long)n + kRsTile - 1) / kRsTile);
     int rc;
-    if ((passes > 1 && ((rc = ensure(h, h->rsKeys, (size_t)n * 4)) || (rc = ensure(h, h->rsVals, (size_t)n * 4)))) ||
-        (rc = ensure(h, h->rsHist, ((size_t)nTiles * 256 + 256) * 4)))
+    if ((passes > 1 && ((rc = ensure(h, sKeys, (size_t)n * 4)) || (rc = ensure(h, sVals, (size_t)n * 4)))) ||
+        (rc = ensure(h, sHist, ((size_t)nTiles * 256 + 256) * 4)))
         return rc;
-    int* hist = P<int>(h->rsHist);
+    int* hist = P<int>(sHist);
     int* digitTot = hist + (size_t)nTiles * 256;
     const unsigned* ki = kin;
     const int* vi = vin;
@@ -284,8 +287,8 @@ int rs_sort_pairs(mas_context* h, const unsigned* kin, unsigned* kout, const int
         const int shift = p * per, nb = std::min(per, bits - shift);
         // the last pass writes kout; earlier ones alternate back from it
         const bool toOut = (passes - 1 - p) % 2 == 0;
-        unsigned* ko = toOut ? kout : P<unsigned>(h->rsKeys);
-        int* vo = toOut ? vout : P<int>(h->rsVals);
+        unsigned* ko = toOut ? kout : P<unsigned>(sKeys);
+        int* vo = toOut ? vout : P<int>(sVals);
         k_rs_count<<<nTiles, kRsThreads, 0, s>>>(ki, n, shift, nb, hist, nTiles);
         k_rs_digit_scan<<<1 << nb, kRsThreads, 0, s>>>(hist, nTiles, digitTot);
         k_rs_scatter<<<nTiles, kRsThreads, 0, s>>>(ki, vi, ko, vo, n, shift, nb, hist, digitTot, nTiles);
@@ -295,15 +298,16 @@ int rs_sort_pairs(mas_context* h, const unsigned* kin, unsigned* kout, const int
     return hip_check(h, hipGetLastError(), what);
 }
 
-int rs_exclusive_scan(mas_context* h, const int* in, int* out, int n, hipStream_t s, const char* what) {
+int rs_exclusive_scan(mas_context* h, const int* in, int* out, int n, hipStream_t s, const char* what, bool side) {
     if (n <= 0) return MAS_OK;
     const int nb = (int)(((long long)n + kScanTile - 1) / kScanTile);
     const bool vec = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
     int* part = nullptr;
     if (nb > 1) {
-        int rc = ensure(h, h->rsPart, (size_t)nb * 4);
+        Buffer& sPart = side ? h->rsPartP : h->rsPart;
+        int rc = ensure(h, sPart, (size_t)nb * 4);
         if (rc) return rc;
-        part = P<int>(h->rsPart);
+        part = P<int>(sPart);
         if (vec) k_scan_reduce<true><<<nb, kScanThreads, 0, s>>>(in, n, part);
         else k_scan_reduce<false><<<nb, kScanThreads, 0, s>>>(in, n, part);
         k_scan_top<<<1, 1024, 0, s>>>(part, nb);
