@@ -358,6 +358,12 @@ void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float
                      P<float4>(h->Zc), h->levelSize[3], z, nullptr, nullptr);
 }
 
+// the coarse form an apply uses: the env / config choice, else the one-launch
+// tagged form at L = 3 (256k: 34.3 -> 32.3 us per apply) and the two-launch
+// form at L >= 4, where the one-launch form measured from 2 us faster to 6 us
+// slower at 1M depending on the box
+int coarse_mode(const mas_context* h) { return h->coarseMode >= 0 ? h->coarseMode : (h->L == 3 ? 3 : 2); }
+
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     if (h->L >= 4 && !h->deepOff.p) return fail(h, MAS_ERR_STATE, "apply: deep-level lists not built");
     if (h->fineBlk0 != 0 || h->fineBlk1 != h->nFineBlk)
@@ -369,11 +375,12 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     // coarse levels (mas_internal.h coarseMode); every form bitwise equal.  The
     // one-launch form's tags carry a host-side epoch, which a graph capture
     // would freeze: a capturing stream gets the two-launch form.
+    const int mode = coarse_mode(h);
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (h->L > 2 && h->coarseMode == 3 && hipStreamIsCapturing(s, &cap) == hipSuccess &&
+    if (h->L > 2 && mode == 3 && hipStreamIsCapturing(s, &cap) == hipSuccess &&
         cap == hipStreamCaptureStatusNone && coarse1_supported(h))
         launch_coarse_one(h, d_r, s);
-    else if (h->L > 2 && h->coarseMode >= 2) launch_coarse_twopass(h, d_r, s);
+    else if (h->L > 2 && mode >= 2) launch_coarse_twopass(h, d_r, s);
     else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
     if (ev) hipEventRecord(ev[1], s);
     launch_fine(h, 0, h->nFineBlk, d_r, d_z, s, h->applyDone, h->applyRzPart);

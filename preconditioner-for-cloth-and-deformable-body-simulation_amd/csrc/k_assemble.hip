@@ -1199,13 +1199,19 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
         fa.coff = P<int>(h->cFineOff);
         fa.B = RecKey::kLaneBits;
     }
-    // od and the record counts need only level-0 data too: computed here on the
-    // whole chip while the levels build, instead of on the caller's reserved CUs
-    if ((rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
-        (rc = hip_check(h, hipMemsetAsync(P<int>(h->recCnt) + nV, 0, 4, ps), "memset recCnt")))
-        return rc;
-    launch_od(h, fa, ps);
-    if ((rc = hip_check(h, hipEventRecord(h->evAdd0, ps), "od ready"))) return rc;
+    // earlyOd (A/B, env MAS_EARLY_OD): od and the record counts need only
+    // level-0 data too and can run here, ahead of the fused kernel, instead of
+    // on the caller's reserved CUs -- which delays the fused kernel, most
+    // often the longer path with 64 CUs reserved
+    h->odDone = false;
+    if (h->earlyOd) {
+        if ((rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
+            (rc = hip_check(h, hipMemsetAsync(P<int>(h->recCnt) + nV, 0, 4, ps), "memset recCnt")))
+            return rc;
+        launch_od(h, fa, ps);
+        h->odDone = true;
+    }
+    if ((rc = hip_check(h, hipEventRecord(h->evAdd0, ps), "add0 ready"))) return rc;
     h->earlyFused = true;
     h->earlyFa = fa;
     return h->fusedAfterLevels ? MAS_OK : launch_level0_fused(h, nullptr);
@@ -1265,7 +1271,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
          (rc = hip_check(h, hipMemsetAsync(static_cast<char*>(h->dense.p) + zeroFrom, 0, coarseBytes, s),
                          "memset dense"))) ||
         (rc = hip_check(h, hipMemsetAsync(h->additional.p, 0, (size_t)(tc + 1) * 36, s), "memset additional")) ||
-        (!h->earlyFused && (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt"))))
+        (!h->odDone && (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt"))))
         return rc;
     float* dense = dense_base(h);
     float* add = P<float>(h->additional);
@@ -1281,12 +1287,12 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         // the level-0 blocks assemble and factor on prepStream while this
         // stream assembles the coarse levels (run_factor joins)
         if (h->earlyFused) {
-            // od and the record counts came with the early path (run_level0_early)
-            if ((rc = hip_check(h, hipStreamWaitEvent(s, h->evAdd0, 0), "wait od"))) return rc;
-        } else {
-            if (!forked && (rc = fork_fused(h, fa, s))) return rc;
-            launch_od(h, fa, s);
+            // add0 (and od, earlyOd) from the early path (run_level0_early)
+            if ((rc = hip_check(h, hipStreamWaitEvent(s, h->evAdd0, 0), "wait add0"))) return rc;
+        } else if (!forked && (rc = fork_fused(h, fa, s))) {
+            return rc;
         }
+        if (!h->odDone) launch_od(h, fa, s);
     } else {
         k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
                                                   d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt),

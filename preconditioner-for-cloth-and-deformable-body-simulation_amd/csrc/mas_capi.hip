@@ -156,6 +156,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_PREP_CU_RESERVE")) h->prepCuReserve = std::atoi(v);
     if (const char* v = std::getenv("MAS_FUSED_AFTER_LEVELS")) h->fusedAfterLevels = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_THREAD")) h->earlyThread = std::atoi(v);
+    if (const char* v = std::getenv("MAS_EARLY_OD")) h->earlyOd = std::atoi(v);
     int rc = upload_slot_table(h);
     if (rc != MAS_OK) {
         mas_destroy(h);
@@ -382,7 +383,7 @@ int mas_get_stats(mas_handle h, mas_stats* out) {
         h->stats.fine_ms_avg = sf / n;
         h->stats.post_fine_ms_avg = sc / n;
     }
-    h->stats.apply_mode = h->coarseMode;
+    h->stats.apply_mode = coarse_mode(h);
     *out = h->stats;
     return MAS_OK;
 }

@@ -121,7 +121,7 @@ struct mas_context {
     // hand-offs (k_coarse1.hip, L >= 3); 2 = two launches, restrictions then
     // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (The
     // side-stream overlap was measured slower: DESIGN.md section 4.)
-    int coarseMode = 3;
+    int coarseMode = -1;  // -1: 3 at L = 3, 2 at L >= 4 (measured)
     // coarse launches in their occupancy forms (k_coarse.hip): -1 = when the
     // level-1 level has >= kCoarseOccBlocks blocks, 0 = never, 1 = always;
     // env MAS_COARSE_OCC
@@ -165,6 +165,8 @@ struct mas_context {
     int prepCuReserve = 64;  // CUs the fused kernel's queue leaves to the caller's stream (env MAS_PREP_CU_RESERVE)
     int fusedAfterLevels = 0;  // A/B (env MAS_FUSED_AFTER_LEVELS): the early fused kernel waits for the level build
     int earlyThread = 1;       // the early path queued from a second host thread (env MAS_EARLY_THREAD)
+    int earlyOd = 0;           // A/B (env MAS_EARLY_OD): k_od in the early path
+    bool odDone = false;       // this Prepare's od / record counts are queued already
     mas::FineAsm earlyFa{};    // its inputs, kept for launch_level0_fused
     hipEvent_t evAdd0 = nullptr;
     mas::Buffer add0, c0Cnt, c0Off, c0Keys, c0KeysS, c0Ids, c0IdsS, c0Val, a0Keys, a0KeysS, a0Ids, a0IdsS, a0Val;
@@ -287,6 +289,7 @@ int run_factor(mas_context* h, hipStream_t s);
 // fused level-0 assemble + factor of blocks [blk0, blk1) (k_factor.hip)
 int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s);
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s);
+int coarse_mode(const mas_context* h);  // the coarse launch form an apply uses (k_apply.hip)
 int upload_slot_table(mas_context* h);
 int prepare_apply_tables(mas_context* h, hipStream_t s);
 int build_l1src(mas_context* h, hipStream_t s);
