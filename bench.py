@@ -423,7 +423,10 @@ def main():
             "fine_solve": round(st["fine_ms_avg"], 5),
             "post_fine": round(st["post_fine_ms_avg"], 5),
             "events_total": round(st["apply_ms_avg"], 5),
-            "coarse_launches": {0: "one per level", 2: "two (k_restrict12, k_solve123)", 3: "one (k_coarse1, tagged hand-offs)"}[st["apply_mode"]],
+            "coarse_launches": ("none (one level)" if info["num_levels"] <= 1 else
+                                "one per level" if info["num_levels"] == 2 else
+                                {0: "one per level", 2: "two (k_restrict12, k_solve123)",
+                                 3: "one (k_coarse1, tagged hand-offs)"}[st["apply_mode"]]),
             "ms_per_step_with_kernel_events": round(elapsed_ev / args.steps * 1e3, 5),
         },
         "apply_algorithmic_GBps": round(apply_bytes / (t_max / args.steps) / 1e9, 1),
