@@ -65,7 +65,7 @@ def test_prepare_schedules_bitwise(kind, W, L, nc, monkeypatch):
     blob_ref, z_ref = ref.save_blob(), _z(ref, r)
     for env in VARIANTS[1:]:
         P = _prepared(mesh, L, contacts, env, monkeypatch)
-        assert P.save_blob() == blob_ref, env
+        assert np.array_equal(P.save_blob(), blob_ref), env
         np.testing.assert_array_equal(_z(P, r), z_ref, err_msg=str(env))
     # the late path (level-0 blocks stored, fused kernel forked after the levels)
     K = _prepared(mesh, L, contacts, {}, monkeypatch, keep_blocks=True)
