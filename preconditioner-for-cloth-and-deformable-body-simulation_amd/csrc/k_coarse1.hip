@@ -102,7 +102,6 @@ struct Coarse1Args {
     const int* deepOff;   // list start per level-3 node, + 1
     unsigned epoch;       // this apply's tag
     int nb1;
-    int l1Delay;          // bank waves: s_sleep(32) rounds before the level-1 inverse load (A/B)
     int pollDelay;        // fold / solve waves: s_sleep(64) rounds before the first poll (A/B)
     const int* done;      // PCG: exit at once when set
 };
@@ -186,7 +185,6 @@ __device__ __forceinline__ void bank_wave(const Coarse1Args& a, int B, C1Shared&
     C1_STAMP(1, B, 2);
     // Z1 of the bank's block from the R1 in registers (inverse loaded after the
     // publications, so the restriction's gathers do not queue behind it)
-    for (int d = 0; d < a.l1Delay; ++d) __builtin_amdgcn_s_sleep(32);
     float g[kRecord], tl[3];
     load_record<true>(a.inv, a.begin1 / 32 + B, lane, g, tl);
     const float3 out = block_solve(g, tl, make_float3(__shfl(ax, j), __shfl(ay, j), __shfl(az, j)), lane);
@@ -372,7 +370,6 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.tR2 = t + nList;
     a.tR3 = a.tR2 + ceil32(a.n2);
     a.epoch = h->coarse1Epoch;
-    a.l1Delay = h->c1L1Delay;
     a.pollDelay = h->c1PollDelay;
     a.done = h->applyDone;
     k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3, 64, 0, s>>>(a);

@@ -187,7 +187,6 @@ struct mas_context {
     // list slot); the apply epoch the tags carry (0 after Prepare)
     mas::Buffer c1Tags, l1info;
     unsigned coarse1Epoch = 0;
-    int c1L1Delay = 0;  // A/B (env MAS_C1_L1DELAY): bank waves sleep before the level-1 inverse load
     int c1PollDelay = 0;  // A/B (env MAS_C1_POLL_DELAY): fold / solve waves sleep before their first poll
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form

@@ -131,6 +131,9 @@ int main() {
             hipMemcpy(c, dc, 16, hipMemcpyDeviceToHost);
             if (c[0] < best) { best = c[0]; rt = c[1]; }
         }
+        float o[3];
+        hipMemcpy(o, dout, 12, hipMemcpyDeviceToHost);
+        printf("  acc %08x %08x %08x\n", *(unsigned*)&o[0], *(unsigned*)&o[1], *(unsigned*)&o[2]);
         printf("%-34s %8llu cycles for %d dependent adds = %.2f cycles/add, %.2f us (%.2f ns/add)\n", name, best, N,
                (double)best / N, rt / 100.0, rt * 10.0 / N);
     };
