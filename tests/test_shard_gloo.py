@@ -2,11 +2,13 @@
 
 Each rank plans its Morton range with the library's host-only planner
 (mas_shard_plan), restricts its own level-1 segment, allgathers the padded
-segments over gloo, solves the coarse levels and its own fine blocks, and
-writes z for its own vertices.  The local arithmetic is a numpy restatement of
-the GPU kernels (float32, same accumulation order) driven by the oracle's maps
-and block inverses; the assembled z must equal the oracle's single-process
-apply.  This covers the N > 1 host logic; the kernels themselves are covered
+segments over gloo, builds the coarse residual hierarchy in the reference's
+order (level 1 from the gathered segments, levels 2-3 as left folds of R1 over
+the level-1 ids, fp32) -- bitwise the oracle's m_mappedR -- solves the coarse
+levels and its own fine blocks, and writes z for its own vertices.  The local
+arithmetic is a numpy restatement of the GPU kernels driven by the oracle's
+maps and block inverses; the assembled z must equal the oracle's
+single-process apply.  This covers the N > 1 host logic; the kernels themselves are covered
 by tests/test_gpu_shard.py (virtual shards on one GPU).
 """
 import os
@@ -69,17 +71,30 @@ def _worker(rank, world, port, W, L, out_dir):
         seg[i, :3] = acc
     gathered = [torch.zeros(plan["seg_max"], 4) for _ in range(world)]
     dist.all_gather(gathered, torch.from_numpy(seg))
-    # unpack (k_unpack_r1) with every rank's plan
-    R = np.zeros((o.total_clusters, 3), np.float64)
+    # unpack (the gathered segments through every rank's plan)
+    R = np.zeros((o.total_clusters, 3), np.float32)
     for g in range(world):
         pg = mas_amd.shard_plan(nV, l1_first, g, world)
         cnt = pg["l1_end"] - pg["l1_begin"]
         R[begin1 + pg["l1_begin"]: begin1 + pg["l1_end"]] = gathered[g].numpy()[:cnt, :3]
-    # levels >= 2 from level-1 (redundant on every rank)
-    for l in range(2, Lv):
-        beg_prev, cnt_prev = int(ls[l - 1][1]), int(ls[l - 1][0])
-        for c in range(beg_prev, beg_prev + cnt_prev):
-            R[gn[c]] += R[c]
+    # levels 2 .. min(L-1, 3) in the reference's order (BuildResidualHierarchy,
+    # .cpp:1577-1590): walking the level-1 ids in order, each R1 is added into
+    # every ancestor, in fp32 -- the order the library's coarse kernels keep
+    # (redundant on every rank); level 4 is never prolonged (B-6) and skipped
+    if Lv > 2:
+        n1 = int(ls[1][0])
+        for c in range(begin1, begin1 + n1):
+            a = c
+            for _ in range(2, min(Lv, 4)):
+                a = int(gn[a])
+                R[a] = (R[a] + R[c]).astype(np.float32)
+    # the residual hierarchy is bitwise the oracle's (m_mappedR)
+    o.apply(r)
+    Ro = o.mapped_r()
+    for l in range(1, min(Lv, 4)):
+        b, n = int(ls[l][1]), int(ls[l][0])
+        assert np.array_equal(R[b:b + n].view(np.uint32), Ro[b:b + n, :3].astype(np.float32).view(np.uint32)), l
+    R = R.astype(np.float64)
     Z = np.zeros_like(R)
     for blk in range(o.total_clusters // 32):
         if blk < nb and not (plan["fine_block_begin"] <= blk < plan["fine_block_end"]):
