@@ -32,8 +32,9 @@
 // product sums the per-workgroup partials itself, in the same fixed order in
 // every workgroup (no single-workgroup "finish" launches), so a solve is
 // run-to-run deterministic.  The scalars (rz, |r|^2, the stop flag) live in
-// device memory: the host enqueues iterations in chunks and reads the state
-// once per chunk; every kernel of a finished solve exits at its first
+// device memory: the host enqueues iterations in chunks and reads the done
+// flag once per chunk, one chunk behind (pinned read-back words, so the queue
+// never drains); every kernel of a finished solve exits at its first
 // instruction.
 //
 // SpMV: G lanes per row (G = 8 for the cloth valence, 16/32 above), lane j
@@ -48,6 +49,7 @@
 // Every kernel, the apply's included, exits at its first instruction once the
 // solve is done, so the chunks enqueued past convergence cost launches only.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "mas_internal.h"
@@ -675,6 +677,18 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     }
     k_pcg_rz<<<g, b, 0, s>>>(nV, r, z, p, st, part);
     k_pcg_rz0<<<1, b, 0, s>>>(st, part);
+    // The host looks at the done flag once per chunk of iterations, one chunk
+    // behind: chunk c + 1 is queued before the flag of chunk c is read
+    // (through the pinned read-back words, no stream synchronisation), so
+    // the GPU never idles on the host's check.  The price is one queued
+    // chunk after convergence, whose kernels return at once on st->done.
+    // MAS_PCG_LAG=0 selects the synchronous check (A/B).
+    static const int lag = [] {
+        const char* v = std::getenv("MAS_PCG_LAG");
+        return v ? std::atoi(v) : 1;
+    }();
+    int pendingSeq = 0;
+    bool pending = false;
     const int chunk = 4;
     for (int it = 0; it < maxIters; it += chunk) {
         for (int k = it; k < it + chunk && k < maxIters; ++k) {
@@ -687,6 +701,17 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
                 k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st, rzPart);
             }
             k_pcg_update_p<<<g, b, 0, s>>>(nV, k, z, p, st, part, rzPart, nRz);
+        }
+        if (lag) {
+            int seq = 0, done = 0;
+            if ((rc = read_back_post(h, s, {&st->done}, &seq))) return rc;
+            if (pending) {
+                if ((rc = read_back_wait(h, s, pendingSeq, &done, 1))) return rc;
+                if (done) break;
+            }
+            pendingSeq = seq;
+            pending = true;
+            continue;
         }
         if ((rc = hip_check(h, hipMemcpyAsync(&host, st, sizeof(host), hipMemcpyDeviceToHost, s), "D2H pcg state")) ||
             (rc = hip_check(h, hipStreamSynchronize(s), "pcg sync")))

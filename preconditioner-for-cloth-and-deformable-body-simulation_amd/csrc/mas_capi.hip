@@ -67,7 +67,7 @@ __global__ void k_readback(ReadBackArgs a, int* host, int seq) {
     __hip_atomic_store(host, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* out) {
+int read_back_post(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* seqOut) {
     if (src.size() > 8) return fail(h, MAS_ERR_ARG, "read_back: at most 8 words");
     if (!h->rbHost) {
         void* p = nullptr;
@@ -82,18 +82,31 @@ int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> s
     for (const int* p : src) a.src[i++] = p;
     const int seq = ++h->rbSeq;
     k_readback<<<1, 64, 0, s>>>(a, h->rbHost, seq);
-    int rc = hip_check(h, hipGetLastError(), "read-back kernel");
-    if (rc) return rc;
+    *seqOut = seq;
+    return hip_check(h, hipGetLastError(), "read-back kernel");
+}
+
+// Waits until the post of sequence `seq` or a later one has landed: the
+// words then hold that post's values or a newer post's (the caller of a
+// lagged read posts the same sources every time).
+int read_back_wait(mas_context* h, hipStream_t s, int seq, int* out, int n) {
+    auto landed = [&] { return __atomic_load_n(h->rbHost, __ATOMIC_ACQUIRE) - seq >= 0; };
     const auto t0 = std::chrono::steady_clock::now();
-    while (__atomic_load_n(h->rbHost, __ATOMIC_ACQUIRE) != seq) {
+    while (!landed()) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-            if ((rc = hip_check(h, hipStreamSynchronize(s), "read-back sync"))) return rc;
-            if (__atomic_load_n(h->rbHost, __ATOMIC_ACQUIRE) != seq) return fail(h, MAS_ERR_HIP, "read-back lost");
+            int rc = hip_check(h, hipStreamSynchronize(s), "read-back sync");
+            if (rc) return rc;
+            if (!landed()) return fail(h, MAS_ERR_HIP, "read-back lost");
             break;
         }
     }
-    for (int k = 0; k < a.n; ++k) out[k] = __atomic_load_n(h->rbHost + 1 + k, __ATOMIC_RELAXED);
+    for (int k = 0; k < n; ++k) out[k] = __atomic_load_n(h->rbHost + 1 + k, __ATOMIC_RELAXED);
     return MAS_OK;
+}
+
+int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* out) {
+    int seq = 0, rc = read_back_post(h, s, src, &seq);
+    return rc ? rc : read_back_wait(h, s, seq, out, (int)src.size());
 }
 
 static void release(Buffer& b) {

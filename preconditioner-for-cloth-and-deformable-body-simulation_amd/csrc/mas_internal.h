@@ -319,6 +319,10 @@ int fine_grid(const mas_context* h);  // workgroups of one fine launch over ever
 int compute_l1_first(mas_context* h, hipStream_t s);
 // up to 8 device ints -> out, through pinned memory (mas_capi.hip)
 int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* out);
+// the same split in two: enqueue the copy (its sequence number in *seq), and
+// later wait for it (or a newer post) to land
+int read_back_post(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* seq);
+int read_back_wait(mas_context* h, hipStream_t s, int seq, int* out, int n);
 void release_comm(mas_context* h);  // comm_rccl.hip
 int copy_block_inverse(mas_context* h, int blk, float* out96);
 int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,
