@@ -44,7 +44,10 @@ extern "C" {
  *    first_pass_iterations, replacements) and gained a reserved tail, so later
  *    additions do not change their size again; mas_config.reference_formation;
  *    MAS_ERR_COMM. */
-#define MAS_ABI_VERSION 2
+/* 3: MAS_ERR_NOT_SPD; mas_stats' reserved tail now carries hier_dirty_level,
+ *    hier_rebuilt, prepare_fine_start_ms, nonspd_blocks, wait_timeouts (same
+ *    size). */
+#define MAS_ABI_VERSION 3
 
 typedef enum {
     MAS_OK = 0,
@@ -55,7 +58,11 @@ typedef enum {
     MAS_ERR_LEVELS = -5,   /* more than 5 levels requested (reference B-6)        */
     MAS_ERR_NOMEM = -6,    /* device allocation failed                           */
     MAS_ERR_NO_DEVICE = -7, /* no HIP device / kernels not loadable               */
-    MAS_ERR_COMM = -8       /* the allgather hook / RCCL failed (see mas_last_error) */
+    MAS_ERR_COMM = -8,      /* the allgather hook / RCCL failed (see mas_last_error) */
+    MAS_ERR_NOT_SPD = -9    /* Prepare: a block's LDL^T met a zero, negative or non-finite pivot
+                               (mas_stats.nonspd_blocks; mas_last_error names the first block).  The
+                               reference divides by such pivots unchecked (.cpp:1406,1431); here the
+                               handle stays prepared with the same inverses, but the call fails */
 } mas_status;
 
 typedef struct mas_context* mas_handle;
@@ -112,7 +119,16 @@ typedef struct {
     double prepare_fine_ms;
     int64_t factor_formation;  /* level-0 inverse formation of the last Prepare: 1 = matrix cores
                                   (v_mfma_f32_32x32x2_f32), 0 = vector ALUs in the reference's order */
-    int64_t reserved[8];       /* zero; room for later fields without a size change */
+    /* incremental level maps (ABI 3): the contact-free hierarchy of the current sort is kept; the last
+       Prepare's contact stencils changed level hier_dirty_level of it (num_levels: none -- its levels,
+       coarse records, term lists and apply tables were reused; -1: not checked, the cache is off) */
+    int64_t hier_dirty_level;
+    int64_t hier_rebuilt;      /* the last Prepare ran a level build (first Prepare after a sort, or dirty) */
+    double prepare_fine_start_ms; /* the fused level-0 kernel's start, after the Prepare's start */
+    int64_t nonspd_blocks;     /* the last Prepare: blocks whose factor met a zero / negative / non-finite pivot */
+    int64_t wait_timeouts;     /* since mas_create: bounded device waits of the one-launch coarse form that
+                                  gave up (the apply's z is then incomplete); mas_apply fails on one */
+    int64_t reserved[3];       /* zero; room for later fields without a size change */
 } mas_stats;
 
 /* lifecycle */
@@ -305,6 +321,13 @@ int mas_get_coarse_residual(mas_handle h, float* out4);
 int mas_dev_sort_pairs(mas_handle h, const unsigned* d_keys_in, unsigned* d_keys_out, const int* d_vals_in,
                        int* d_vals_out, int n, int bits, int impl);
 int mas_dev_exclusive_scan(mas_handle h, const int* d_in, int* d_out, int n, int impl);
+/* The contact Hessian terms the assembly kernels use (.cpp:1190,1208-1223),
+ * for n stencils given by direction dir3[n][3], stiffness stiff[n] and five
+ * weights w5[n][5] (host arrays): out[n][234], column-major 3x3 each --
+ * OuterProduct(d, d * stiff), H * Square(w[it]) for it < 5, and per pair
+ * a < b < 5 w[a] * w[b] * H, then the same times 2.0f (tests pin them against
+ * the reference's own headers). */
+int mas_dev_contact_terms(mas_handle h, const float* dir3, const float* stiff, const float* w5, float* out, int n);
 
 #ifdef __cplusplus
 }

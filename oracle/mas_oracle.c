@@ -591,6 +591,41 @@ static int reorder_realtime(orc_state* s) {
 /* Prepare: Hessian assembly, .cpp:1164-1345                           */
 /* ------------------------------------------------------------------ */
 
+/* The contact terms of one stencil (.cpp:1208-1223), column-major 3x3:
+ *   contact_outer   hessian = OuterProduct(d, d * stiff)   SeMatrix.h:352-363,
+ *                   SeVector.h:250 (d * stiff lane by lane)
+ *   contact_self    hessian * Math::Square(w)              SeMath.h:98, SeMatrix.h:741
+ *   contact_pair    w_a * w_b * hessian                    SeMatrix.h:977 (scalar * mat = mat * scalar)
+ *   contact_double  t * 2.0f                               .cpp:1190
+ * Shared by prepare_collision_hessian and orc_contact_terms (the fixture check
+ * against the reference's own headers, tests/test_ref_pinned.py). */
+static void contact_outer(const float* dir, float stiff, float* h) {
+    const float ds[3] = {dir[0] * stiff, dir[1] * stiff, dir[2] * stiff};
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) h[c * 3 + r] = dir[r] * ds[c];
+}
+static void contact_self(const float* h, float w, float* t) {
+    const float w2 = w * w;
+    for (int e = 0; e < 9; ++e) t[e] = h[e] * w2;
+}
+static void contact_pair(const float* h, float wa, float wb, float* t) {
+    const float ww = wa * wb;
+    for (int e = 0; e < 9; ++e) t[e] = ww * h[e];
+}
+static void contact_double(const float* t, float* t2) {
+    for (int e = 0; e < 9; ++e) t2[e] = t[e] * 2.0f;
+}
+
+void orc_contact_terms(const float* dir3, float stiff, const float* w5, float* out) {
+    contact_outer(dir3, stiff, out);
+    for (int it = 0; it < 5; ++it) contact_self(out, w5[it], out + 9 + 9 * it);
+    for (int a = 0, p = 0; a < 5; ++a)
+        for (int b = a + 1; b < 5; ++b, ++p) {
+            contact_pair(out, w5[a], w5[b], out + 54 + 9 * p);
+            contact_double(out + 54 + 9 * p, out + 144 + 9 * p);
+        }
+}
+
 /* AdditionalSchwarzHessian2, .cpp:1164-1199 */
 static void additional_schwarz_hessian2(orc_state* s, const float* h, int v1, int v2) {
     int level = 0;
@@ -609,7 +644,7 @@ static void additional_schwarz_hessian2(orc_state* s, const float* h, int v1, in
         ot = (unsigned)s->goingNext[ot];
         if (my == ot) {
             float h2[9];
-            for (int i = 0; i < 9; ++i) h2[i] = h[i] * 2.0f;
+            contact_double(h, h2);
             m3_add(s->additional + 9 * (size_t)my, h2);
         } else {
             m3_add(s->additional + 9 * (size_t)my, h);
@@ -623,20 +658,17 @@ static void prepare_collision_hessian(orc_state* s) {
     for (int i = 0; i < s->nStencil; ++i) {
         const orc_stencil* st = &s->stencils[i];
         const int* idx = s->stencilIdx + 5 * (size_t)i;
-        float d[3] = {st->dir[0], st->dir[1], st->dir[2]};
-        float ds[3] = {d[0] * st->stiff, d[1] * st->stiff, d[2] * st->stiff};
         float h[9]; /* OuterProduct(d, d*stiff), SeMatrix.h:352-363; column-major */
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) h[c * 3 + r] = d[r] * ds[c];
+        contact_outer(st->dir, st->stiff, h);
         for (int it = 0; it < st->n; ++it) {
-            float w2 = st->weight[it] * st->weight[it], t[9];
-            for (int e = 0; e < 9; ++e) t[e] = h[e] * w2;
+            float t[9];
+            contact_self(h, st->weight[it], t);
             m3_add(s->additional + 9 * (size_t)idx[it], t);
         }
         for (int a = 0; a < st->n; ++a)
             for (int b = a + 1; b < st->n; ++b) {
-                float ww = st->weight[a] * st->weight[b], t[9];
-                for (int e = 0; e < 9; ++e) t[e] = ww * h[e];
+                float t[9];
+                contact_pair(h, st->weight[a], st->weight[b], t);
                 additional_schwarz_hessian2(s, t, idx[a], idx[b]);
             }
     }

@@ -93,6 +93,12 @@ uint64_t orc_morton_encode(float x, float y, float z);
 float orc_clamp(float a, float lo, float hi); /* Math::Clamp, SeMath.h:103 */
 float orc_min(float a, float b);              /* Math::Min, SeMath.h:101 */
 float orc_max(float a, float b);              /* Math::Max, SeMath.h:102 */
+/* The contact Hessian terms of one stencil (.cpp:1208-1223) from direction
+ * dir3, stiffness and five weights; out[234], column-major 3x3 each: [0, 9)
+ * H = OuterProduct(d, d * stiff), [9 + 9 it] H * Square(w[it]) (it < 5),
+ * [54 + 9 p] w[a] * w[b] * H and [144 + 9 p] that times 2.0f, pairs p over
+ * a < b < 5 in (a, b) order. */
+void orc_contact_terms(const float* dir3, float stiff, const float* w5, float* out);
 
 #ifdef __cplusplus
 }

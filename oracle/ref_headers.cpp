@@ -19,9 +19,16 @@
 //   * memory layouts of SeMatrix3f (SeMatrix.h:650-682), Int4 (SeVector.h:395),
 //     Float2/Float3/Float4 and SeCsr<int> (SeCsr.h:35-173) with Size / IdxPtr.
 //
+//   * the contact Hessian terms of PrepareCollisionHessian /
+//     AdditionalSchwarzHessian2 (SeSchwarzPreconditioner.cpp:1190,1208-1223):
+//     the same expressions on the reference's own types -- Float3 d * stiff
+//     (SeVector.h:250), OuterProduct (SeMatrix.h:352-363), Math::Square
+//     (SeMath.h:98), SeMatrix3f * scalar and scalar * SeMatrix3f
+//     (SeMatrix.h:741,977) -- written by element accessor (i, j).
+//
 // What it cannot pin: SeVec3fSimd and the contact records (SeVectorSimd.h and
 // SeCollisionElements.h need a source patch of SeVectorSimd.h:101-102 to
-// compile) and the .cpp's floating-point phases (same patch + MSVC
+// compile) and the .cpp's other floating-point phases (same patch + MSVC
 // <intrin.h>); see DESIGN.md section 2.
 #include <math.h>
 
@@ -150,6 +157,28 @@ int refh_csr_probe(const int* starts, int rows, const int* idx, int* sizes, long
     }
     *total = c.Size();
     return c.Rows();
+}
+
+// The contact terms of one stencil, as .cpp:1208-1223 and :1190 write them
+// (the weights come from the stencil; here any five): out[234] column-major
+// 3x3 each -- [0, 9) hessian = OuterProduct(d, d * s.stiff); [9 + 9 it]
+// hessian * Math::Square(w[it]); [54 + 9 p] w[a] * w[b] * hessian and
+// [144 + 9 p] that * 2.0f, pairs p over a < b < 5 in (a, b) order.
+void refh_contact_terms(const float* dir3, float stiff, const float* w, float* out) {
+    auto put = [&](const SE::SeMatrix3f& m, float* dst) {
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) dst[j * 3 + i] = m(i, j);
+    };
+    SE::Float3 d(dir3[0], dir3[1], dir3[2]);
+    SE::SeMatrix3f hessian = SE::OuterProduct(d, d * stiff);
+    put(hessian, out);
+    for (int it = 0; it < 5; ++it) put(hessian * SE::Math::Square(w[it]), out + 9 + 9 * it);
+    for (int a = 0, p = 0; a < 5; ++a)
+        for (int b = a + 1; b < 5; ++b, ++p) {
+            SE::SeMatrix3f t = w[a] * w[b] * hessian;
+            put(t, out + 54 + 9 * p);
+            put(t * 2.0f, out + 144 + 9 * p);
+        }
 }
 
 }  // extern "C"

@@ -251,6 +251,10 @@ int blob_load(mas_context* h, const void* src, size_t size) {
     // commit: adopt the sizes, then upload every section
     h->prepared = false;
     h->allocated = false;
+    // the restored maps are a hierarchy of their own: nothing cached applies
+    h->meshHierValid = h->liveIsMesh = false;
+    h->hierId = ++h->hierCounter;
+    h->recHierId = ~0ull;
     h->nV = hd.nV; h->nE = hd.nE; h->nF = hd.nF; h->L = hd.L; h->natL = hd.natL;
     h->totalClusters = hd.totalClusters; h->nBlk = hd.nBlk; h->nFineBlk = hd.nFineBlk;
     h->fineBlk0 = 0; h->fineBlk1 = hd.nFineBlk;  // a blob holds every block's inverse
@@ -278,6 +282,7 @@ int blob_load(mas_context* h, const void* src, size_t size) {
     if ((rc = build_l1src(h, h->stream)) || (rc = hip_check(h, hipStreamSynchronize(h->stream), "blob sync")))
         return rc;
     h->shardWorld = 0;
+    h->tabHierId = h->hierId;
     h->fromBlob = true;
     h->allocated = true;  // maps are valid
     h->prepared = true;

@@ -192,6 +192,8 @@ int run_allocate(mas_context* h, const float* pos4, const int* starts, const int
         h->allocated = true;
         return hip_check(h, hipStreamSynchronize(s), "allocate sync");
     }
+    // a new vertex order: the cached contact-free hierarchy (and all derived from it) is stale
+    h->meshHierValid = h->liveIsMesh = false;
     hipEventRecord(h->ev[0], s);
     if ((rc = ensure(h, h->aabbPartial, (size_t)(2 * kAabbGrid + 2) * 16)) ||
         (rc = ensure(h, h->morton, (size_t)nV * 8)) || (rc = ensure(h, h->mortonSorted, (size_t)nV * 8)) ||

@@ -105,10 +105,47 @@ __device__ __forceinline__ void add_colmajor(float* e, const float* __restrict__
 //                 ascending), folded into the target's diagonal
 // Contact-free inputs skip all of it.
 
-__device__ __forceinline__ void contact_h(const DevStencil& s, float (&hm)[9]) {
+// The contact terms (.cpp:1190,1208-1223), column-major 3x3; pinned bit for
+// bit against the reference's own headers (mas_dev_contact_terms,
+// tests/test_gpu_ref_pinned.py; fixtures tests/golden/ref_contact.npz).
+__device__ __forceinline__ void contact_outer(const float* dir, float stiff, float (&hm)[9]) {
     // OuterProduct(d, d * stiff), SeMatrix.h:352-363; column-major: hm[c * 3 + r] = d_r (d_c stiff)
     for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) hm[c * 3 + r] = __fmul_rn(s.dir[r], __fmul_rn(s.dir[c], s.stiff));
+        for (int c = 0; c < 3; ++c) hm[c * 3 + r] = __fmul_rn(dir[r], __fmul_rn(dir[c], stiff));
+}
+__device__ __forceinline__ void contact_h(const DevStencil& s, float (&hm)[9]) { contact_outer(s.dir, s.stiff, hm); }
+// hessian * Math::Square(w), SeMath.h:98 / SeMatrix.h:741
+__device__ __forceinline__ void contact_self(const float (&hm)[9], float w, float* out) {
+    const float w2 = __fmul_rn(w, w);
+    for (int e = 0; e < 9; ++e) out[e] = __fmul_rn(hm[e], w2);
+}
+// w_a * w_b * hessian, SeMatrix.h:977
+__device__ __forceinline__ void contact_pair(const float (&hm)[9], float wa, float wb, float (&t)[9]) {
+    const float ww = __fmul_rn(wa, wb);
+    for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e]);
+}
+// AdditionalSchwarzHessian2's hessian * 2.0f (.cpp:1190)
+__device__ __forceinline__ float contact_double(float t) { return __fmul_rn(t, 2.0f); }
+
+// mas_dev_contact_terms: the terms of n stencils (orc_contact_terms layout, 234 floats each)
+__global__ __launch_bounds__(64) void k_contact_terms(const float* __restrict__ dir3, const float* __restrict__ stiff,
+                                                      const float* __restrict__ w5, int n, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float hm[9], t[9];
+    contact_outer(dir3 + 3 * (size_t)i, stiff[i], hm);
+    float* o = out + 234 * (size_t)i;
+    for (int e = 0; e < 9; ++e) o[e] = hm[e];
+    const float* w = w5 + 5 * (size_t)i;
+    for (int it = 0; it < 5; ++it) contact_self(hm, w[it], o + 9 + 9 * it);
+    for (int a = 0, p = 0; a < 5; ++a)
+        for (int b = a + 1; b < 5; ++b, ++p) {
+            contact_pair(hm, w[a], w[b], t);
+            for (int e = 0; e < 9; ++e) {
+                o[54 + 9 * p + e] = t[e];
+                o[144 + 9 * p + e] = contact_double(t[e]);
+            }
+        }
 }
 
 // counts: dCnt[i] block-entry records, aCnt[i] additional records of stencil i
@@ -153,19 +190,17 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
     contact_h(s, hm);
     int d = dOff[i], a = aOff[i];
     for (int it = 0; it < s.n && !skip0; ++it, ++a) {  // .cpp:1214-1217: additional[idx] += h w^2
-        const float w2 = __fmul_rn(s.w[it], s.w[it]);
         aKeys[a] = (unsigned)s.idx[it];
         aIds[a] = a;
-        for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = __fmul_rn(hm[e], w2);
+        contact_self(hm, s.w[it], aVal + 9 * (size_t)a);
     }
     for (int x = 0; x < s.n; ++x)
         for (int y = x + 1; y < s.n; ++y) {
             unsigned my = (unsigned)s.idx[x], ot = (unsigned)s.idx[y];
             const int level = climb(gn, L, my, ot);
             if (level >= L) continue;
-            const float ww = __fmul_rn(s.w[x], s.w[y]);
             float t[9];
-            for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e]);
+            contact_pair(hm, s.w[x], s.w[y], t);
             if (level > 0 || !skip0) {
                 // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot]
                 dKeys[d] = (EntryKey)((my << 5) | (ot & 31u));
@@ -180,7 +215,7 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
                 if (pm == po) {
                     aKeys[a] = pm;
                     aIds[a] = a;
-                    for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = __fmul_rn(t[e], 2.0f);
+                    for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = contact_double(t[e]);
                     ++a;
                 } else {
                     aKeys[a] = pm;
@@ -226,19 +261,17 @@ __global__ __launch_bounds__(256) void k_contact0_write(const DevStencil* __rest
     contact_h(s, hm);
     for (int it = 0; it < s.n; ++it) {  // .cpp:1214-1217: additional[idx] += h w^2
         const int a = kA0 * i + it;
-        const float w2 = __fmul_rn(s.w[it], s.w[it]);
         aKeys[a] = (unsigned)s.idx[it];
         aIds[a] = a;
-        for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = __fmul_rn(hm[e], w2);
+        contact_self(hm, s.w[it], aVal + 9 * (size_t)a);
     }
     int d = dOff[i];
     for (int x = 0; x < s.n; ++x)
         for (int y = x + 1; y < s.n; ++y) {
             const unsigned my = (unsigned)s.idx[x], ot = (unsigned)s.idx[y];
             if ((my >> 5) != (ot >> 5)) continue;
-            const float ww = __fmul_rn(s.w[x], s.w[y]);
             float t[9];
-            for (int e = 0; e < 9; ++e) t[e] = __fmul_rn(ww, hm[e]);
+            contact_pair(hm, s.w[x], s.w[y], t);
             dKeys[d] = (EntryKey)((my << 5) | (ot & 31u));
             dKeys[d + 1] = (EntryKey)((ot << 5) | (my & 31u));
             dIds[d] = d;
@@ -1140,7 +1173,7 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
     // coarse share like the previous Prepare's (run_assemble grows it keeping
     // the level-0 part if the hierarchy needs more)
     const size_t blockBytes = (size_t)kBlockFloats * 4;
-    const size_t want = (size_t)std::max(h->nBlk, h->nFineBlk + h->nFineBlk / 8 + 64) * blockBytes;
+    const size_t want = (size_t)std::max(h->nBlkPrev, h->nFineBlk + h->nFineBlk / 8 + 64) * blockBytes;
     if (h->inv.bytes < (size_t)h->nFineBlk * blockBytes && (rc = ensure(h, h->inv, want))) return rc;
     if ((rc = ensure(h, h->add0, (size_t)nv32 * 36))) return rc;
     // evPrepFork was recorded on s right after the stencils (run_prepare), before
@@ -1300,15 +1333,12 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     }
     if (L == 1) return hip_check(h, hipGetLastError(), "assembly kernels");
 
-    // coarse edge records in (u, k) order
-    if ((rc = exclusive_scan(h, P<int>(h->recCnt), P<int>(h->recOff), nV + 1, s, "record scan"))) return rc;
-    int nRec = 0;
-    if ((rc = read_back(h, s, {P<int>(h->recOff) + nV}, &nRec))) return rc;
-    const size_t nr = nRec > 0 ? nRec : 1;
-    if ((rc = ensure(h, h->rec, nr * sizeof(EdgeRec))) || (rc = ensure(h, h->recKeys, nr * 4)) ||
-        (rc = ensure(h, h->recKeysSorted, nr * 4)) || (rc = ensure(h, h->recIds, nr * 4)) ||
-        (rc = ensure(h, h->recIdsSorted, nr * 4)))
-        return rc;
+    // Coarse edge records, their stable sort and the diagTable term lists
+    // depend only on the hierarchy and the CSR structure, not on any value: a
+    // Prepare whose hierarchy is the one they were built for (and whose CSR
+    // ranges equal the ones they index off9 with) reuses them and only folds.
+    const bool cached = h->hierCache && h->recHierId == h->hierId && !h->rangesChanged;
+    h->recHierId = ~0ull;  // valid again only once rebuilt below
     EdgeRec* rec = P<EdgeRec>(h->rec);
     const RecKey rk{h->levelSize[3], bit_width((unsigned)(tc - h->levelSize[3]))};
     if (rk.bits() > 32) return fail(h, MAS_ERR_ARG, "record keys: more than 2^27 coarse nodes");
@@ -1316,6 +1346,40 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     const int valence = h->maxNbr - 1;
     const int lanesPerVertex = valence <= 8 ? 8 : valence <= 16 ? 16 : valence <= 32 ? 32 : 64;
     if (valence > 64) return fail(h, MAS_ERR_ARG, "more than 64 neighbours per vertex");
+    if (cached) {
+        const int nRec = h->nRecCached;
+        if (nRec > 0)
+            k_fold_runs<DenseEntry, true, EntryKey><<<cdiv(nRec, 64), 64, 0, s>>>(
+                nRec, rk.dead(), P<EntryKey>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
+                DenseEntry{dense, rk});
+        k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
+        for (int l = 2; l < L; ++l) {
+            const int count = h->levelSize[2 * l], begin = h->levelSize[2 * l + 1];
+            const int beginPrev = h->levelSize[2 * (l - 1) + 1];
+            if (count > 0)
+                k_table_fold<<<count, 64, 0, s>>>(l, count, begin, beginPrev, P<int>(h->vlistL[l]),
+                                                  P<int>(h->voffL[l]), P<int>(h->termOffL[l]), P<int>(h->termsL[l]),
+                                                  P<int>(h->cst) + (size_t)(l - 2) * nV, gn, d_off9, P<float>(h->od),
+                                                  P<float>(h->tab), dense);
+        }
+        h->recHierId = h->hierId;
+        return hip_check(h, hipGetLastError(), "assembly kernels");
+    }
+
+    // coarse edge records in (u, k) order
+    if ((rc = exclusive_scan(h, P<int>(h->recCnt), P<int>(h->recOff), nV + 1, s, "record scan"))) return rc;
+    int nRec = 0;
+    if ((rc = read_back(h, s, {P<int>(h->recOff) + nV}, &nRec))) return rc;
+    const size_t nr = nRec > 0 ? nRec : 1;
+    if ((rc = ensure(h, h->rec, nr * sizeof(EdgeRec))) || (rc = ensure(h, h->recKeys, nr * 4)) ||
+        (rc = ensure(h, h->recKeysSorted, nr * 4)) || (rc = ensure(h, h->recIds, nr * 4)) ||
+        (rc = ensure(h, h->recIdsSorted, nr * 4)) || (rc = ensure(h, h->recRanges, (size_t)(nV + 1) * 4)))
+        return rc;
+    rec = P<EdgeRec>(h->rec);
+    // the ranges these records index off9 with (k_hier_check compares the next Prepare's)
+    if ((rc = hip_check(h, hipMemcpyAsync(h->recRanges.p, d_ranges, (size_t)(nV + 1) * 4, hipMemcpyDeviceToDevice, s),
+                        "keep ranges")))
+        return rc;
     auto recordLaunch = [&](auto gtag) {
         constexpr int G = decltype(gtag)::value;
         k_records<G><<<cdiv(nV * G, 256), 256, 0, s>>>(nV, L, rk, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr),
@@ -1342,49 +1406,76 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     }
     k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
 
-    // diagTable folds, levels 2..L-1
-    if ((rc = ensure(h, h->vkeys, (size_t)nV * 4)) || (rc = ensure(h, h->vlist, (size_t)nV * 4)) ||
-        (rc = ensure(h, h->voff, (size_t)(nV + 1) * 4)) || (rc = ensure(h, h->termCnt, (size_t)(nV + 1) * 4)) ||
-        (rc = ensure(h, h->termOff, (size_t)(nV + 1) * 4)) || (rc = ensure(h, h->terms, ((size_t)nRec + nV) * 4)))
-        return rc;
+    // diagTable folds, levels 2..L-1 (term lists kept per level for the next Prepare)
+    if ((rc = ensure(h, h->vkeys, (size_t)nV * 4)) || (rc = ensure(h, h->termCnt, (size_t)(nV + 1) * 4))) return rc;
     for (int l = 2; l < L; ++l) {
         const int count = h->levelSize[2 * l], begin = h->levelSize[2 * l + 1];
         const int beginPrev = h->levelSize[2 * (l - 1) + 1];
         const int* cstPrev = P<int>(h->cst) + (size_t)(l - 1) * nV;  // level-l local id per vertex
         const int* cstPrev2 = P<int>(h->cst) + (size_t)(l - 2) * nV; // level-(l-1) local id per vertex
+        if ((rc = ensure(h, h->vlistL[l], (size_t)nV * 4)) || (rc = ensure(h, h->voffL[l], (size_t)(nV + 1) * 4)) ||
+            (rc = ensure(h, h->termOffL[l], (size_t)(nV + 1) * 4)) ||
+            (rc = ensure(h, h->termsL[l], ((size_t)nRec + nV) * 4)))
+            return rc;
+        int* vlist = P<int>(h->vlistL[l]);
+        int* voff = P<int>(h->voffL[l]);
+        int* termOff = P<int>(h->termOffL[l]);
+        int* terms = P<int>(h->termsL[l]);
         // keys are level-l local ids < count: sort only their bits
         const int vbits = std::max(1, bit_width((unsigned)std::max(count - 1, 0)));
         if ((rc = sort_pairs(h, reinterpret_cast<const unsigned*>(cstPrev), P<unsigned>(h->vkeys), P<int>(h->iota),
-                             P<int>(h->vlist), nV, vbits, s, "vertex-list sort")))
+                             vlist, nV, vbits, s, "vertex-list sort")))
             return rc;
-        k_bounds<<<cdiv(nV, 256), 256, 0, s>>>(nV, P<int>(h->vkeys), count, P<int>(h->voff));
-        k_term_count<<<cdiv(nV + 1, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff), rec,
-                                                       P<int>(h->termCnt));
-        if ((rc = exclusive_scan(h, P<int>(h->termCnt), P<int>(h->termOff), nV + 1, s, "term scan"))) return rc;
+        k_bounds<<<cdiv(nV, 256), 256, 0, s>>>(nV, P<int>(h->vkeys), count, voff);
+        k_term_count<<<cdiv(nV + 1, 256), 256, 0, s>>>(l, nV, vlist, P<int>(h->recOff), rec, P<int>(h->termCnt));
+        if ((rc = exclusive_scan(h, P<int>(h->termCnt), termOff, nV + 1, s, "term scan"))) return rc;
         switch (lanesPerVertex) {
             case 8:
-                k_term_write<<<cdiv(nV, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff), rec,
-                                                           P<int>(h->termOff), P<int>(h->terms));
+                k_term_write<<<cdiv(nV, 256), 256, 0, s>>>(l, nV, vlist, P<int>(h->recOff), rec, termOff, terms);
                 break;
             case 16:
-                k_term_write_lanes<16><<<cdiv(nV * 16, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff),
-                                                                          rec, P<int>(h->termOff), P<int>(h->terms));
+                k_term_write_lanes<16><<<cdiv(nV * 16, 256), 256, 0, s>>>(l, nV, vlist, P<int>(h->recOff), rec,
+                                                                          termOff, terms);
                 break;
             case 32:
-                k_term_write_lanes<32><<<cdiv(nV * 32, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff),
-                                                                          rec, P<int>(h->termOff), P<int>(h->terms));
+                k_term_write_lanes<32><<<cdiv(nV * 32, 256), 256, 0, s>>>(l, nV, vlist, P<int>(h->recOff), rec,
+                                                                          termOff, terms);
                 break;
             default:
-                k_term_write_lanes<64><<<cdiv(nV * 64, 256), 256, 0, s>>>(l, nV, P<int>(h->vlist), P<int>(h->recOff),
-                                                                          rec, P<int>(h->termOff), P<int>(h->terms));
+                k_term_write_lanes<64><<<cdiv(nV * 64, 256), 256, 0, s>>>(l, nV, vlist, P<int>(h->recOff), rec,
+                                                                          termOff, terms);
                 break;
         }
         if (count > 0)
-            k_table_fold<<<count, 64, 0, s>>>(l, count, begin, beginPrev, P<int>(h->vlist), P<int>(h->voff),
-                                              P<int>(h->termOff), P<int>(h->terms), cstPrev2, gn, d_off9,
-                                              P<float>(h->od), P<float>(h->tab), dense);
+            k_table_fold<<<count, 64, 0, s>>>(l, count, begin, beginPrev, vlist, voff, termOff, terms, cstPrev2, gn,
+                                              d_off9, P<float>(h->od), P<float>(h->tab), dense);
     }
+    h->nRecCached = nRec;
+    h->recHierId = h->hierId;
     return hip_check(h, hipGetLastError(), "assembly kernels");
 }
 
 }  // namespace mas
+
+int mas_dev_contact_terms(mas_handle h, const float* dir3, const float* stiff, const float* w5, float* out, int n) {
+    using namespace mas;
+    if (!h || n < 0 || (n > 0 && (!dir3 || !stiff || !w5 || !out))) return MAS_ERR_ARG;
+    if (n == 0) return MAS_OK;
+    hipSetDevice(h->device);
+    Buffer b;
+    const size_t inF = (size_t)n * 9, outF = (size_t)n * 234;
+    int rc = hip_check(h, hipMalloc(&b.p, (inF + outF) * 4), "hipMalloc");
+    if (rc) return rc;
+    float* d = static_cast<float*>(b.p);
+    hipStream_t s = h->stream;
+    if (!(rc = hip_check(h, hipMemcpyAsync(d, dir3, (size_t)n * 12, hipMemcpyHostToDevice, s), "H2D")) &&
+        !(rc = hip_check(h, hipMemcpyAsync(d + 3 * n, stiff, (size_t)n * 4, hipMemcpyHostToDevice, s), "H2D")) &&
+        !(rc = hip_check(h, hipMemcpyAsync(d + 4 * n, w5, (size_t)n * 20, hipMemcpyHostToDevice, s), "H2D"))) {
+        k_contact_terms<<<cdiv(n, 64), 64, 0, s>>>(d, d + 3 * n, d + 4 * n, n, d + inF);
+        if (!(rc = hip_check(h, hipGetLastError(), "contact terms")))
+            rc = hip_check(h, hipMemcpyAsync(out, d + inF, outF * 4, hipMemcpyDeviceToHost, s), "D2H");
+    }
+    hipStreamSynchronize(s);
+    hipFree(b.p);
+    return rc;
+}

@@ -63,7 +63,6 @@ __device__ unsigned long long g_probe1[3 * 8192 * 8];
 #endif
 
 constexpr int kFoldStep = 512;     // list entries polled per fold step (8 per lane)
-constexpr int kPollLimit = 1 << 16;  // bounded waits: never hang the device
 
 // x, y, z of one hand-off, one tagged 64-bit word each (TagWord)
 struct Tag3 {
@@ -104,6 +103,8 @@ struct Coarse1Args {
     int nb1;
     int pollDelay;        // fold / solve waves: s_sleep(64) rounds before the first poll (A/B)
     const int* done;      // PCG: exit at once when set
+    int pollLimit;        // polls before a wait gives up (kPollLimit; < 0: give up at once, a test knob)
+    int* timeouts;        // waits that gave up: this apply's z is incomplete (mas_stats.wait_timeouts)
 };
 
 union C1Shared {
@@ -225,7 +226,10 @@ __device__ __forceinline__ void fold_wave(const Coarse1Args& a, int T, C1Shared&
         for (int o = 32; o > 0; o >>= 1) bad = min(bad, __shfl_xor(bad, o));
         const int p = min(bad, n);
         if (p == 0) {
-            if (++idle > kPollLimit) break;  // never hang: leave the fold incomplete
+            if (a.pollLimit < 0 || ++idle > a.pollLimit) {  // never hang: the fold stays incomplete, and says so
+                if (lane == 0) atomicAdd(a.timeouts, 1);
+                break;
+            }
             __builtin_amdgcn_s_sleep(2);
             poll(e);
             continue;
@@ -273,7 +277,7 @@ __device__ __forceinline__ void solve_wave(const Coarse1Args& a, int blk, int lv
     unsigned long long v[3] = {0ull, 0ull, 0ull};
     bool ok = !real;
     for (int d = 0; d < a.pollDelay; ++d) __builtin_amdgcn_s_sleep(64);
-    for (int polls = 0; polls <= kPollLimit; ++polls) {
+    for (int polls = 0; polls <= a.pollLimit; ++polls) {
         if (!ok) {
             ld_tag(tR + loc, v);
             ok = tag_ok(v, a.epoch);
@@ -281,6 +285,7 @@ __device__ __forceinline__ void solve_wave(const Coarse1Args& a, int blk, int lv
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
     }
+    if (!__all(ok) && lane == 0) atomicAdd(a.timeouts, 1);  // solved from stale R: counted
     C1_STAMP(2, slot, 1);
     // half 1 takes node n's residual from lane n (padding nodes: +0)
     const float rx = __shfl(tag_val(v[0]), n), ry = __shfl(tag_val(v[1]), n), rz = __shfl(tag_val(v[2]), n);
@@ -372,6 +377,9 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.epoch = h->coarse1Epoch;
     a.pollDelay = h->c1PollDelay;
     a.done = h->applyDone;
+    a.pollLimit = h->c1PollLimit;
+    a.timeouts = P<int>(h->devStatus) + 2;
+    h->c1Launched = true;
     k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3, 64, 0, s>>>(a);
 }
 

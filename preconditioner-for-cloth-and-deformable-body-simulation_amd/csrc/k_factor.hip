@@ -34,9 +34,24 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef float v2f __attribute__((ext_vector_type(2)));
 static_assert(kDenseFloats / 4 % kFactorThreads == 0, "factor load tiling");
 
+// Failure detection (the reference divides by every pivot unchecked,
+// .cpp:1406,1431): a block whose D^-1 holds a zero, negative or non-finite
+// entry -- a zero / negative / non-finite pivot, or one so small that its
+// reciprocal overflows -- is counted in status[0] and the lowest such block
+// kept in status[1] (MAS_ERR_NOT_SPD after Prepare).  One wave, lanes 0..63
+// read D^-1 entries lane and 64 + lane; the inverses are unchanged.
+__device__ __forceinline__ void check_pivots(const float* dinv, int* status, int blk, int lane) {
+    const float d0 = dinv[lane], d1 = lane < 32 ? dinv[64 + lane] : 1.f;
+    const bool bad = !(d0 > 0.f && d0 <= 3.402823466e38f) || !(d1 > 0.f && d1 <= 3.402823466e38f);
+    if (__ballot(bad) && lane == 0) {
+        atomicAdd(status, 1);
+        atomicMin(status + 1, blk);
+    }
+}
+
 __global__ __launch_bounds__(kFactorThreads) void k_factor(const float* __restrict__ dense,
                                                           const unsigned* __restrict__ slotTable,
-                                                          float* __restrict__ inv, int blk0) {
+                                                          float* __restrict__ inv, int blk0, int* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) float A[96 * kLda];
     __shared__ float dinv[96];
     const int t = threadIdx.x;
@@ -75,6 +90,7 @@ __global__ __launch_bounds__(kFactorThreads) void k_factor(const float* __restri
     }
     if (t < 96) dinv[t] = __fdiv_rn(1.0f, A[t * kLda + t]);
     __syncthreads();
+    if (status && t < 64) check_pivots(dinv, status, (int)blk, t);
     float* out = inv + blk * kBlockFloats;
     for (int o = t; o < kBlockFloats; o += kFactorThreads) {
         const unsigned ij = slotTable[o];
@@ -374,7 +390,7 @@ __device__ __forceinline__ void form_mfma(float* M, const float* dinv, float* ou
 template <bool MFMA>
 __device__ __forceinline__ void factor_tiles(float (&v)[6][24], float* M, float* piv, float* dinv, float* out,
                                              const uint4* __restrict__ tileSlot, const uint4* __restrict__ valuSlot,
-                                             int t) {
+                                             int t, int* status, int blk) {
     const int rg = t >> 2, cg = t & 3;
     ElimRB<0>::run(v, piv, dinv, rg, cg);
     // M rows: unit diagonal, L^-1 below, only the stored (padded) columns
@@ -398,6 +414,7 @@ __device__ __forceinline__ void factor_tiles(float (&v)[6][24], float* M, float*
         }
     }
     __syncthreads();
+    if (status) check_pivots(dinv, status, blk, t);
     if (MFMA) form_mfma(M, dinv, out, tileSlot, t);  // one wave: no barrier around M
     else form_packed_staged(M, dinv, out, valuSlot, t);
 }
@@ -409,7 +426,7 @@ __device__ __forceinline__ void factor_tiles(float (&v)[6][24], float* M, float*
 template <bool MFMA>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_rb(
     const float* __restrict__ dense, float* __restrict__ inv, const uint4* __restrict__ tileSlot,
-    const uint4* __restrict__ valuSlot, int blk0) {
+    const uint4* __restrict__ valuSlot, int blk0, int* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) float M[kPackedM];
     __shared__ __attribute__((aligned(16))) float piv[96];
     __shared__ float dinv[96];
@@ -431,7 +448,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 v[m][4 * c4 + 3] = q.w;
             }
     }
-    factor_tiles<MFMA>(v, M, piv, dinv, inv + blk * kBlockFloats, tileSlot, valuSlot, t);
+    factor_tiles<MFMA>(v, M, piv, dinv, inv + blk * kBlockFloats, tileSlot, valuSlot, t, status, (int)blk);
 }
 
 // ---------------------------------------------------------------------------
@@ -555,7 +572,7 @@ __device__ __forceinline__ void slab_to_tiles(float (&v)[6][24], const float* S,
 template <bool MFMA>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_fused(
     FineAsm a, float* __restrict__ inv, const uint4* __restrict__ tileSlot, const uint4* __restrict__ valuSlot,
-    int blk0) {
+    int blk0, int* __restrict__ status) {
     static_assert(48 * 96 <= kPackedM, "a slab fits in M's LDS");
     __shared__ __attribute__((aligned(16))) float M[kPackedM];
     __shared__ __attribute__((aligned(16))) float piv[96];
@@ -571,17 +588,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     slab_to_tiles<1>(v, M, t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    factor_tiles<MFMA>(v, M, piv, dinv, inv + (size_t)blk * kBlockFloats, tileSlot, valuSlot, t);
+    factor_tiles<MFMA>(v, M, piv, dinv, inv + (size_t)blk * kBlockFloats, tileSlot, valuSlot, t, status, blk);
 }
 
 int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s) {
     // MAS_FACTOR_VARIANT=5: the matrix-core formation (form_mfma, not bitwise)
     if (blk1 > blk0 && h->factorVariant == 5)
         k_factor_fused<true><<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
-                                                        P<uint4>(h->valuSlot), blk0);
+                                                        P<uint4>(h->valuSlot), blk0, P<int>(h->devStatus));
     else if (blk1 > blk0)
         k_factor_fused<false><<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
-                                                         P<uint4>(h->valuSlot), blk0);
+                                                         P<uint4>(h->valuSlot), blk0, P<int>(h->devStatus));
     return hip_check(h, hipGetLastError(), "fused factor kernel");
 }
 
@@ -650,18 +667,18 @@ int run_factor(mas_context* h, hipStream_t s) {
         const int b0 = rg[0], nb = rg[1] - rg[0];
         if (nb <= 0) continue;
         if (h->factorVariant == 0) {
-            k_factor<<<nb, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv, b0);
+            k_factor<<<nb, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv, b0, P<int>(h->devStatus));
         } else {
             k_identity_fix<<<cdiv(nb * 32, 256), 256, 0, s>>>(dense, b0 * 32, rg[1] * 32);
             if (h->factorVariant == 3)
-                k_factor_rb<true><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0);
+                k_factor_rb<true><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0,
+                                                    P<int>(h->devStatus));
             else
-                k_factor_rb<false><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0);
+                k_factor_rb<false><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0,
+                                                     P<int>(h->devStatus));
         }
     }
-    int rc = hip_check(h, hipGetLastError(), "factor kernel");
-    if (!rc && fused) rc = hip_check(h, hipStreamWaitEvent(s, h->evPrepJoin, 0), "join fused factor");
-    return rc;
+    return hip_check(h, hipGetLastError(), "factor kernel");  // run_prepare joins the fused kernel
 }
 
 }  // namespace mas

@@ -277,6 +277,58 @@ __global__ __launch_bounds__(256) void k_vertex_maps(int nV, int L, const int* _
 }
 
 // ---------------------------------------------------------------------------
+// incremental level maps: do the contact stencils change the mesh hierarchy?
+// ---------------------------------------------------------------------------
+//
+// The level-(l+1) nodes are the connected components, inside each level-l
+// bank, of the mesh edges plus the contact pairs mapped to level l
+// (BuildCollisionConnection .cpp:514-563 ORs a stencil's first x second
+// primitive pairs into the connect masks).  While levels 0..l-1 are unchanged
+// (same ids as the contact-free hierarchy), the mesh edges at level l are the
+// contact-free ones, so level l changes iff some pair maps to two different
+// nodes of one bank that lie in different contact-free components -- the
+// pair's bit is missing from the closed mask of its first node.  A pair that
+// joins nodes of one component merges nothing and maps to one node above.
+// flag[0] = the lowest level a pair changes (atomicMin; init >= L: none).
+struct HierCheckArgs {
+    const unsigned* fine;         // closed level-0 masks (contact-free)
+    const unsigned* coarseMask;   // closed masks of levels >= 1 at (begin_l - nv32) + local id
+    const int* cst;               // contact-free CoarseSpaceTables [L][nV]
+    int maskBase[kMaxLevels];     // begin_l - nv32 (l >= 1)
+    int L, nV;
+};
+__global__ __launch_bounds__(256) void k_hier_check(const DevStencil* __restrict__ st, int n, HierCheckArgs a,
+                                                    int* __restrict__ flag) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const DevStencil s = st[i];
+    int dirty = a.L;
+    for (int x = 0; x < s.nFirst; ++x)
+        for (int y = s.nFirst; y < s.n; ++y) {
+            const int vx = s.idx[x], vy = s.idx[y];
+            for (int l = 0; l < a.L && l < dirty; ++l) {
+                const unsigned my = l ? (unsigned)a.cst[(size_t)(l - 1) * a.nV + vx] : (unsigned)vx;
+                const unsigned ot = l ? (unsigned)a.cst[(size_t)(l - 1) * a.nV + vy] : (unsigned)vy;
+                if (my == ot) break;             // one node from here up
+                if ((my >> 5) != (ot >> 5)) continue;  // not connected at this level
+                const unsigned m = l ? a.coarseMask[a.maskBase[l] + my] : a.fine[my];
+                if (!((m >> (ot & 31)) & 1u)) dirty = l;  // joins two components
+                break;                           // same component: one node above
+            }
+        }
+    if (dirty < a.L) atomicMin(flag, dirty);
+}
+
+// flag |= (a != b) over n ints: the CSR ranges the cached coarse records index
+// off9 with, against this Prepare's
+__global__ __launch_bounds__(256) void k_ranges_differ(const int* __restrict__ a, const int* __restrict__ b, int n,
+                                                       int* __restrict__ flag) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool d = i < n && a[i] != b[i];
+    if (__ballot(d) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+// ---------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------
 
@@ -356,11 +408,19 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
     return hip_check(h, hipGetLastError(), "stencil kernels");
 }
 
-// ReorderRealtime, .cpp:415-445
-int run_levels(mas_context* h, hipStream_t s, const std::function<int()>& beforeRead) {
+// ReorderRealtime, .cpp:415-445; contacts = false: the contact-free (mesh)
+// hierarchy, the stencils ignored
+static int build_levels(mas_context* h, hipStream_t s, const std::function<int()>& beforeRead, bool contacts) {
     const int nV = h->nV, L = h->L, nv32 = ceil32(nV);
     const int nB0 = nv32 / 32;
+    const int nSt = contacts ? h->nStencil : 0;
     int rc;
+    // .cpp:74-75: fresh copies of the ELL neighbour table (compacted level by level below)
+    if ((rc = hip_check(h, hipMemcpyAsync(h->nbrRem.p, h->nbr.p, (size_t)h->maxNbr * nV * 4, hipMemcpyDeviceToDevice, s),
+                        "copy nbr")) ||
+        (rc = hip_check(h, hipMemcpyAsync(h->nbrNumRem.p, h->nbrNum.p, (size_t)nV * 4, hipMemcpyDeviceToDevice, s),
+                        "copy nbrNum")))
+        return rc;
     if ((rc = ensure(h, h->fineMask, (size_t)nv32 * 4)) || (rc = ensure(h, h->nextMask, (size_t)nv32 * 4)) ||
         (rc = ensure(h, h->bankCount, (size_t)(nB0 + 1) * 4)) || (rc = ensure(h, h->bankPrefix, (size_t)(nB0 + 1) * 4)) ||
         (rc = ensure(h, h->levelTotal, 16 * 4)) || (rc = ensure(h, h->cst, (size_t)L * nV * 4)) ||
@@ -382,7 +442,7 @@ int run_levels(mas_context* h, hipStream_t s, const std::function<int()>& before
 
     // level 0 -> 1
     k_connect_l0<<<g, 256, 0, s>>>(nV, P<int>(h->nbrNumRem), P<int>(h->nbrRem), fine);
-    if (h->nStencil) k_collision_connect<<<cdiv(h->nStencil, 256), 256, 0, s>>>(st, h->nStencil, nullptr, fine);
+    if (nSt) k_collision_connect<<<cdiv(nSt, 256), 256, 0, s>>>(st, nSt, nullptr, fine);
     k_bank_closure<<<cdiv(nV, 256), 256, 0, s>>>(nV, tot, 0, nv32, fine, cnt, nullptr);
     if ((rc = scan_counts(h, cnt, pre, nB0, s))) return rc;
     k_assign_ids<<<cdiv(nV, 256), 256, 0, s>>>(nV, 0, nv32, fine, pre, cnt, cst, gn, tot);
@@ -394,11 +454,11 @@ int run_levels(mas_context* h, hipStream_t s, const std::function<int()>& before
         const int* prev = cst + (size_t)(level - 1) * nV;
         if ((rc = hip_check(h, hipMemsetAsync(next, 0, (size_t)nv32 * 4, s), "memset nextMask"))) return rc;
         k_connect_lx<<<g, 256, 0, s>>>(nV, prev, P<int>(h->nbrNumRem), P<int>(h->nbrRem), next);
-        if (h->nStencil) k_collision_connect<<<cdiv(h->nStencil, 256), 256, 0, s>>>(st, h->nStencil, prev, next);
-        // keeps the level-l component masks (the apply's child lists) before
-        // k_assign_ids overwrites them with ids
-        k_bank_closure<<<cdiv(nV, 256), 256, 0, s>>>(0, tot, level, nv32, next, cnt,
-                                                     level + 1 < L ? P<unsigned>(h->coarseMask) : nullptr);
+        if (nSt) k_collision_connect<<<cdiv(nSt, 256), 256, 0, s>>>(st, nSt, prev, next);
+        // keeps the level-l component masks (the apply's child lists, and the
+        // contact check's closed masks, k_hier_check) before k_assign_ids
+        // overwrites them with ids
+        k_bank_closure<<<cdiv(nV, 256), 256, 0, s>>>(0, tot, level, nv32, next, cnt, P<unsigned>(h->coarseMask));
         if ((rc = scan_counts(h, cnt, pre, nB0, s))) return rc;
         k_assign_ids<<<cdiv(nV, 256), 256, 0, s>>>(0, level, nv32, next, pre, cnt, nullptr, gn, tot);
         k_next_level<<<g, 256, 0, s>>>(nV, prev, next, cst + (size_t)level * nV);
@@ -418,6 +478,98 @@ int run_levels(mas_context* h, hipStream_t s, const std::function<int()>& before
     h->nFineBlk = nv32 / 32;
     k_vertex_maps<<<g, 256, 0, s>>>(nV, L, P<int>(h->s2o), gn, P<int4>(h->coarseTables), P<int4>(h->vmap));
     return hip_check(h, hipGetLastError(), "level kernels");
+}
+
+// the hierarchy maps of the live slot <-> the spare slot (mas_context)
+static void swap_hier_slots(mas_context* h) {
+    std::swap(h->cst, h->spCst);
+    std::swap(h->goingNext, h->spGn);
+    std::swap(h->vmap, h->spVmap);
+    std::swap(h->coarseTables, h->spCoarseTables);
+    std::swap(h->fineMask, h->spFine);
+    std::swap(h->coarseMask, h->spCoarseMask);
+}
+
+// Incremental level maps: the contact-free hierarchy is built
+// once per sort; a Prepare whose stencils do not change it (k_hier_check, one
+// host read) reuses it as is, and everything derived from it alone (records,
+// term lists, apply tables: hierId) is reused too; otherwise the levels are
+// rebuilt with the contacts, the contact-free hierarchy kept in the spare
+// slot.  Either way the maps equal a full rebuild's, bit for bit.
+int run_levels(mas_context* h, hipStream_t s, const int* d_ranges, const std::function<int()>& beforeRead) {
+    const int L = h->L, nV = h->nV, nv32 = ceil32(nV);
+    int rc;
+    h->rangesChanged = true;
+    h->lastHierBuilt = true;  // until a reuse below says otherwise
+    if (!h->hierCache) {  // A/B (MAS_HIER_CACHE=0): the full build every Prepare
+        h->meshHierValid = h->liveIsMesh = false;
+        h->hierId = ++h->hierCounter;
+        h->lastHierDirty = -1;
+        return build_levels(h, s, beforeRead, true);
+    }
+    bool hooked = false;
+    auto hook = [&]() -> int {
+        if (hooked || !beforeRead) return MAS_OK;
+        hooked = true;
+        return beforeRead();
+    };
+    bool justBuilt = false;
+    if (!h->meshHierValid) {  // first Prepare after a sort: the contact-free hierarchy
+        justBuilt = true;
+        if ((rc = build_levels(h, s, hook, false))) return rc;
+        std::copy(h->levelSize, h->levelSize + 18, h->meshLevelSize);
+        h->meshHierValid = h->liveIsMesh = true;
+        h->meshHierId = h->hierId = ++h->hierCounter;
+        h->lastHierDirty = L;
+        if (h->nStencil == 0) return hook();
+    }
+    // does this Prepare's contact set change it?  (and do the CSR ranges
+    // differ from the ones the cached records index off9 with?)
+    const bool live = h->liveIsMesh;
+    const bool wantRanges = h->recHierId == h->meshHierId && h->recRanges.bytes >= (size_t)(nV + 1) * 4;
+    int flags[2] = {L, 1};
+    if (h->nStencil > 0 || wantRanges) {
+        if ((rc = ensure(h, h->hierFlags, 16))) return rc;
+        int* f = P<int>(h->hierFlags);
+        if ((rc = hip_check(h, hipMemsetD32Async(f, L, 1, s), "hier flags")) ||
+            (rc = hip_check(h, hipMemsetD32Async(f + 1, 0, 1, s), "hier flags")))
+            return rc;
+        if (h->nStencil > 0) {
+            HierCheckArgs a{};
+            a.fine = P<unsigned>(live ? h->fineMask : h->spFine);
+            a.coarseMask = P<unsigned>(live ? h->coarseMask : h->spCoarseMask);
+            a.cst = P<int>(live ? h->cst : h->spCst);
+            for (int l = 1; l < L; ++l) a.maskBase[l] = h->meshLevelSize[2 * l + 1] - nv32;
+            a.L = L;
+            a.nV = nV;
+            k_hier_check<<<cdiv(h->nStencil, 256), 256, 0, s>>>(P<DevStencil>(h->stencils), h->nStencil, a, f);
+        }
+        if (wantRanges)
+            k_ranges_differ<<<cdiv(nV + 1, 256), 256, 0, s>>>(d_ranges, P<int>(h->recRanges), nV + 1, f + 1);
+        if ((rc = hip_check(h, hipGetLastError(), "hierarchy check")) || (rc = hook()) ||
+            (rc = read_back(h, s, {f, f + 1}, flags)))
+            return rc;
+    }
+    if ((rc = hook())) return rc;
+    h->rangesChanged = !wantRanges || flags[1] != 0;
+    if (flags[0] >= L) {  // unchanged: the contact-free hierarchy is this Prepare's
+        h->lastHierBuilt = justBuilt;  // swapping slots is not a build
+        if (!h->liveIsMesh) swap_hier_slots(h);
+        h->liveIsMesh = true;
+        std::copy(h->meshLevelSize, h->meshLevelSize + 18, h->levelSize);
+        h->totalClusters = h->levelSize[2 * L + 1];
+        h->nBlk = h->totalClusters / 32;
+        h->nFineBlk = nv32 / 32;
+        h->hierId = h->meshHierId;
+        h->lastHierDirty = L;
+        return MAS_OK;
+    }
+    // level flags[0] changes: rebuild with the contacts, the contact-free maps kept in the spare slot
+    if (h->liveIsMesh) swap_hier_slots(h);
+    h->liveIsMesh = false;
+    h->lastHierDirty = flags[0];
+    h->hierId = ++h->hierCounter;
+    return build_levels(h, s, {}, true);
 }
 
 }  // namespace mas

@@ -768,7 +768,8 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
         res->first_pass_iterations = host.firstPass;
         res->replacements = host.replacements;
     }
-    return hip_check(h, hipGetLastError(), "pcg kernels");
+    if ((rc = hip_check(h, hipGetLastError(), "pcg kernels"))) return rc;
+    return take_wait_timeouts(h, s);  // a preconditioner apply whose coarse hand-off gave up fails the solve
 }
 
 }  // namespace mas

@@ -17,8 +17,13 @@
 
 namespace mas {
 
+static thread_local std::string* tlErrSink = nullptr;
+ErrorSink::ErrorSink(std::string* sink) { tlErrSink = sink; }
+ErrorSink::~ErrorSink() { tlErrSink = nullptr; }
+
 int fail(mas_context* h, int code, const std::string& msg) {
-    if (h) h->err = msg;
+    if (tlErrSink) *tlErrSink = msg;
+    else if (h) h->err = msg;
     return code;
 }
 
@@ -109,6 +114,22 @@ int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> s
     return rc ? rc : read_back_wait(h, s, seq, out, (int)src.size());
 }
 
+int take_wait_timeouts(mas_context* h, hipStream_t s) {
+    if (!h->c1Launched || !h->devStatus.p) return MAS_OK;
+    h->c1Launched = false;
+    int n = 0;
+    int* w = P<int>(h->devStatus) + 2;
+    int rc;
+    if ((rc = hip_check(h, hipMemcpyAsync(&n, w, 4, hipMemcpyDeviceToHost, s), "read status")) ||
+        (rc = hip_check(h, hipStreamSynchronize(s), "read status")))
+        return rc;
+    if (n == 0) return MAS_OK;
+    h->waitTimeouts += n;
+    if ((rc = hip_check(h, hipMemsetAsync(w, 0, 4, s), "clear status"))) return rc;
+    return fail(h, MAS_ERR_HIP, std::to_string(n) + " bounded hand-off wait(s) of the one-launch coarse form gave "
+                                "up (k_coarse1): the coarse part of z is incomplete");
+}
+
 static void release(Buffer& b) {
     if (b.p) hipFree(b.p);
     b.p = nullptr;
@@ -165,11 +186,19 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_POLL_DELAY")) h->c1PollDelay = std::atoi(v);
+    if (const char* v = std::getenv("MAS_C1_POLL_LIMIT")) h->c1PollLimit = std::atoi(v);
     if (const char* v = std::getenv("MAS_PREP_CU_RESERVE")) h->prepCuReserve = std::atoi(v);
     if (const char* v = std::getenv("MAS_FUSED_AFTER_LEVELS")) h->fusedAfterLevels = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_THREAD")) h->earlyThread = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_OD")) h->earlyOd = std::atoi(v);
+    if (const char* v = std::getenv("MAS_HIER_CACHE")) h->hierCache = std::atoi(v);
+    // MAS_PREP_SERIAL=1 (A/B) queues the early path on the caller's stream: from
+    // one host thread, so the launch order on that stream is fixed
+    if (const char* v = std::getenv("MAS_PREP_SERIAL"))
+        if (std::atoi(v)) h->earlyThread = 0;
     int rc = upload_slot_table(h);
+    if (rc == MAS_OK && (rc = ensure(h, h->devStatus, 16 * sizeof(int))) == MAS_OK)
+        rc = hip_check(h, hipMemset(h->devStatus.p, 0, 16 * sizeof(int)), "device status words");
     if (rc != MAS_OK) {
         mas_destroy(h);
         return rc;
@@ -335,7 +364,8 @@ int mas_apply(mas_handle h, float* z4, const float* r4) {
     MAS_TRY(hip_check(h, hipMemcpyAsync(h->rStage.p, r4, bytes, hipMemcpyHostToDevice, h->stream), "H2D r"));
     MAS_TRY(run_apply(h, P<float4>(h->zStage), P<float4>(h->rStage), h->stream));
     MAS_TRY(hip_check(h, hipMemcpyAsync(z4, h->zStage.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H z"));
-    return hip_check(h, hipStreamSynchronize(h->stream), "apply sync");
+    MAS_TRY(hip_check(h, hipStreamSynchronize(h->stream), "apply sync"));
+    return take_wait_timeouts(h, h->stream);  // a synchronous apply reports an incomplete z
 }
 
 int mas_set_profiling(mas_handle h, int enable) {
@@ -396,6 +426,14 @@ int mas_get_stats(mas_handle h, mas_stats* out) {
         h->stats.post_fine_ms_avg = sc / n;
     }
     h->stats.apply_mode = coarse_mode(h);
+    if (h->c1Launched) {  // the counter of waits that gave up, after every apply queued so far
+        hipSetDevice(h->device);
+        hipDeviceSynchronize();
+        const std::string keep = h->err;
+        take_wait_timeouts(h, h->stream);  // counted here; the error itself is mas_apply's to return
+        h->err = keep;
+    }
+    h->stats.wait_timeouts = h->waitTimeouts;
     *out = h->stats;
     return MAS_OK;
 }

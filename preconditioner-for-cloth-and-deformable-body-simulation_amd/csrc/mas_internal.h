@@ -133,6 +133,7 @@ struct mas_context {
     // 0 = default-policy loads (A/B)
     int fineVariant = 1;
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
+    int nBlkPrev = 0;  // nBlk of the previous Prepare, read by the early path's thread (run_levels may change nBlk meanwhile)
     // sharded Prepare (mas_set_prepare_shard): the next Prepare assembles and
     // factors only the level-0 blocks of Morton shard prepRank / prepWorld;
     // [fineBlk0, fineBlk1) = the level-0 blocks the last Prepare factored
@@ -171,12 +172,39 @@ struct mas_context {
     hipEvent_t evAdd0 = nullptr;
     mas::Buffer add0, c0Cnt, c0Off, c0Keys, c0KeysS, c0Ids, c0IdsS, c0Val, a0Keys, a0KeysS, a0Ids, a0IdsS, a0Val;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
-    mas::Buffer vkeys, vlist, voff, tab, termCnt, termOff, terms;
+    mas::Buffer vkeys, tab, termCnt;
     // contact records (k_assemble.hip): block entries (d*), additional rows (a*), pushes (p*)
     mas::Buffer cdCnt, cdOff, cdKeys, cdKeysS, cdIds, cdIdsS, cdVal, cFineOff;
     mas::Buffer caCnt, caOff, caKeys, caKeysS, caIds, caIdsS, caVal;
     mas::Buffer cpCnt, cpOff, cpKeys, cpKeysS, cpIds, cpIdsS;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, shardPos1, l1src;
+    // Incremental level maps (DESIGN.md section 4 "Prepare").
+    // The contact-free ("mesh") hierarchy of the current sort is built once and
+    // kept; each Prepare checks on the device whether its contact stencils
+    // change it (a pair joining two different mesh components inside a bank at
+    // some level, k_hier_check).  If not, the level build is skipped and so is
+    // everything derived from the hierarchy alone (coarse edge records and
+    // their sort, the diagTable term lists, the apply tables); else the levels
+    // are rebuilt with the contacts.  The hierarchy maps live in two slots: the
+    // live buffers (cst, goingNext, vmap, coarseTables, fineMask, coarseMask)
+    // and a spare set; a dirty Prepare swaps the mesh hierarchy into the spare
+    // slot before rebuilding, a clean one swaps it back (no copies).
+    mas::Buffer spCst, spGn, spVmap, spCoarseTables, spFine, spCoarseMask;
+    bool meshHierValid = false;  // a slot holds the mesh hierarchy of the current sort
+    bool liveIsMesh = false;     // ... and it is the live slot
+    int meshLevelSize[2 * 9] = {};
+    int hierCache = 1;           // env MAS_HIER_CACHE=0: rebuild the levels every Prepare (A/B)
+    unsigned long long hierId = 0, meshHierId = 0, hierCounter = 0;  // identity of the live hierarchy
+    unsigned long long recHierId = ~0ull, tabHierId = ~0ull;  // hierarchy the records / apply tables were built for
+    int nRecCached = 0;
+    int lastHierDirty = -1;      // level the last Prepare's contacts changed (L: none; -1: full build)
+    bool rangesChanged = true;   // this Prepare's CSR ranges differ from recRanges
+    bool lastHierBuilt = false;  // the last Prepare ran a level build
+    mas::Buffer hierFlags;       // device words: [0] first dirty level, [1] ranges differ from recRanges
+    mas::Buffer recRanges;       // the CSR ranges the cached records index off9 with
+    // diagTable term lists per level (cached with the records): vertex list,
+    // its per-node offsets, per-vertex term offsets, terms
+    mas::Buffer vlistL[5], voffL[5], termOffL[5], termsL[5];
     // level-3 descendant lists (k_coarse.hip): sort scratch, list
     // offsets, deepIdx = level-1 id per list slot, deepPos = list slot of
     // every level-1 node, R1 in list order (deepR1), per-block arrival counters
@@ -188,6 +216,14 @@ struct mas_context {
     mas::Buffer c1Tags, l1info;
     unsigned coarse1Epoch = 0;
     int c1PollDelay = 0;  // A/B (env MAS_C1_POLL_DELAY): fold / solve waves sleep before their first poll
+    // k_coarse1's bounded waits never hang the device: a wait gives up after
+    // this many polls and is counted (env MAS_C1_POLL_LIMIT; < 0 forces it: tests)
+    int c1PollLimit = 1 << 16;
+    bool c1Launched = false;    // k_coarse1 ran since devStatus[2] was last read
+    // device status words: [0] blocks with a bad pivot (this Prepare), [1] the
+    // lowest such block, [2] coarse hand-off waits that gave up (since read)
+    mas::Buffer devStatus;
+    long long waitTimeouts = 0;  // [2] accumulated on the host
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
     mas::Buffer pcgRzPart;                               // PCG: r.z partials of the fine apply kernel
@@ -239,13 +275,17 @@ struct mas_context {
                               &stencilSlots, &stencils, &fineMask, &nextMask, &bankCount, &bankPrefix, &levelTotal,
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &tileSlot, &valuSlot, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
-                              &vlist, &voff, &tab, &termCnt, &termOff, &terms,
+                              &tab, &termCnt,
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cFineVal, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
                               &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart, &rsKeysP, &rsValsP, &rsHistP, &rsPartP, &add0, &c0Cnt, &c0Off, &c0Keys, &c0KeysS, &c0Ids, &c0IdsS,
-                              &c0Val, &a0Keys, &a0KeysS, &a0Ids, &a0IdsS, &a0Val};
+                              &c0Val, &a0Keys, &a0KeysS, &a0Ids, &a0IdsS, &a0Val,
+                              &spCst, &spGn, &spVmap, &spCoarseTables, &spFine, &spCoarseMask, &hierFlags, &recRanges,
+                              &devStatus};
         for (mas::Buffer* b : all) f(*b);
+        for (int l = 0; l < 5; ++l)
+            for (mas::Buffer* b : {&vlistL[l], &voffL[l], &termOffL[l], &termsL[l]}) f(*b);
     }
 };
 
@@ -253,6 +293,15 @@ struct mas_context {
 namespace mas {
 
 int fail(mas_context* h, int code, const std::string& msg);
+// While alive, fail() on this host thread stores its message in *sink instead
+// of the handle (a helper thread of one call must not race the caller's
+// writes of mas_context::err).
+struct ErrorSink {
+    explicit ErrorSink(std::string* sink);
+    ~ErrorSink();
+    ErrorSink(const ErrorSink&) = delete;
+    ErrorSink& operator=(const ErrorSink&) = delete;
+};
 int hip_check(mas_context* h, hipError_t e, const char* what);
 int ensure(mas_context* h, Buffer& b, size_t bytes);
 template <class T>
@@ -274,8 +323,9 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
                 hipStream_t s);
 int build_stencils(mas_context* h, const void* ef, const void* ee, const void* vf, const unsigned* efC,
                    const unsigned* eeC, const unsigned* vfC, hipStream_t s);
-// beforeRead: called after the level kernels are queued, before the one host read
-int run_levels(mas_context* h, hipStream_t s, const std::function<int()>& beforeRead = {});
+// the level maps of this Prepare (incremental: k_levels.hip); beforeRead: called
+// once the device work is queued, before the first host read
+int run_levels(mas_context* h, hipStream_t s, const int* d_ranges, const std::function<int()>& beforeRead = {});
 int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s);
 // the level-0 contact path and the fused level-0 kernel on prepStream, right
 // after the stencils (fused variants without keep_blocks); sets earlyFused
@@ -319,6 +369,9 @@ int fine_grid(const mas_context* h);  // workgroups of one fine launch over ever
 int compute_l1_first(mas_context* h, hipStream_t s);
 // up to 8 device ints -> out, through pinned memory (mas_capi.hip)
 int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* out);
+// devStatus[2] (coarse hand-off waits that gave up) -> h->waitTimeouts, after
+// the work that may have set it is complete; MAS_ERR_HIP when new ones came
+int take_wait_timeouts(mas_context* h, hipStream_t s);
 // the same split in two: enqueue the copy (its sequence number in *seq), and
 // later wait for it (or a newer post) to land
 int read_back_post(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* seq);

@@ -14,11 +14,10 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     int rc;
     h->prepared = false;
     hipEventRecord(h->ev[2], s);
-    // .cpp:74-75: fresh copies of the ELL neighbour table
-    if ((rc = hip_check(h, hipMemcpyAsync(h->nbrRem.p, h->nbr.p, (size_t)h->maxNbr * h->nV * 4, hipMemcpyDeviceToDevice, s),
-                        "copy nbr")) ||
-        (rc = hip_check(h, hipMemcpyAsync(h->nbrNumRem.p, h->nbrNum.p, (size_t)h->nV * 4, hipMemcpyDeviceToDevice, s),
-                        "copy nbrNum")))
+    // pivot checks of this Prepare's factors: [0] count, [1] lowest block (k_factor.hip check_pivots)
+    int* status = P<int>(h->devStatus);
+    if ((rc = hip_check(h, hipMemsetD32Async(status, 0, 1, s), "status")) ||
+        (rc = hip_check(h, hipMemsetD32Async(status + 1, 0x7fffffff, 1, s), "status")))
         return rc;
     if ((rc = build_stencils(h, ef, ee, vf, efC, eeC, vfC, s))) return rc;
     ScopedEvents ev;
@@ -34,20 +33,33 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     // prepStream after the stencils (the fork event), beside the level build;
     // their launches are queued while the level kernels run (run_levels' hook)
     h->earlyFused = false;
+    h->nBlkPrev = h->nBlk;
     const bool early = early_fused_wanted(h);
     if (early && ((rc = prep_stream_init(h)) || (rc = hip_check(h, hipEventRecord(h->evPrepFork, s), "fork"))))
         return rc;
     if (early && h->earlyThread) {
         // a second host thread queues prepStream's work while this one queues
         // the level build: each stream is fed from the start (one thread
-        // queueing both left the early path behind the level kernels)
+        // queueing both left the early path behind the level kernels).  HIP's
+        // current device is per host thread: the new thread selects the
+        // handle's first (ensure() allocates on the current device).  Its
+        // error message is stored by this thread after the join.
         int earlyRc = MAS_OK;
-        std::thread t([&]() { earlyRc = run_level0_early(h, d_diag9, d_off9, d_ranges, s); });
-        rc = run_levels(h, s);
+        std::string earlyErr;
+        std::thread t([&]() {
+            if (hipSetDevice(h->device) != hipSuccess) {
+                earlyRc = MAS_ERR_HIP;
+                earlyErr = "early Prepare thread: hipSetDevice failed";
+                return;
+            }
+            ErrorSink sink(&earlyErr);  // fail() from this thread writes earlyErr, not h->err
+            earlyRc = run_level0_early(h, d_diag9, d_off9, d_ranges, s);
+        });
+        rc = run_levels(h, s, d_ranges);
         t.join();
         if (rc) return rc;
-        if (earlyRc) return earlyRc;
-    } else if ((rc = run_levels(h, s, [&]() {
+        if (earlyRc) return fail(h, earlyRc, earlyErr);
+    } else if ((rc = run_levels(h, s, d_ranges, [&]() {
                     return early ? run_level0_early(h, d_diag9, d_off9, d_ranges, s) : MAS_OK;
                 }))) {
         return rc;
@@ -63,9 +75,18 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
         return rc;
     if (nCoarseNodes > 0 && (rc = hip_check(h, hipMemsetAsync(h->Rc.p, 0, (size_t)nCoarseNodes * 16, s), "memset Rc")))
         return rc;
-    if ((rc = prepare_apply_tables(h, s))) return rc;
-    h->l1First.clear();  // per-bank level-1 starts: computed on first use (sharding, blob save)
-    h->shardWorld = 0;
+    // the apply tables depend on the hierarchy alone: kept while it is unchanged
+    if (!h->hierCache || h->tabHierId != h->hierId) {
+        h->tabHierId = ~0ull;
+        if ((rc = prepare_apply_tables(h, s))) return rc;
+        h->tabHierId = h->hierId;
+        h->l1First.clear();  // per-bank level-1 starts: computed on first use (sharding, blob save)
+        h->shardWorld = 0;
+    }
+    // the fused level-0 kernel (prepStream) joins last: nothing above needs
+    // the level-0 inverses
+    if (h->factorVariant >= 4 && (rc = hip_check(h, hipStreamWaitEvent(s, h->evPrepJoin, 0), "join fused factor")))
+        return rc;
     hipEventRecord(h->ev[3], s);
     if ((rc = hip_check(h, hipStreamSynchronize(s), "prepare sync"))) return rc;
     float a = 0, b = 0, c = 0, t = 0;
@@ -77,11 +98,28 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     h->stats.prepare_levels_ms = a;
     h->stats.prepare_assemble_ms = b;
     h->stats.prepare_factor_ms = c;
-    float f = 0;
-    if (h->factorVariant >= 4 && h->evFine[0]) hipEventElapsedTime(&f, h->evFine[0], h->evFine[1]);
+    float f = 0, f0 = 0;
+    if (h->factorVariant >= 4 && h->evFine[0]) {
+        hipEventElapsedTime(&f, h->evFine[0], h->evFine[1]);
+        hipEventElapsedTime(&f0, h->ev[2], h->evFine[0]);
+    }
     h->stats.prepare_fine_ms = f;
+    h->stats.prepare_fine_start_ms = f0;
     h->stats.factor_formation = (h->factorVariant == 5 || h->factorVariant == 3) ? 1 : 0;
-    h->prepared = true;
+    h->stats.hier_dirty_level = h->hierCache ? h->lastHierDirty : -1;
+    h->stats.hier_rebuilt = h->lastHierBuilt ? 1 : 0;
+    int bad[2] = {0, 0};
+    if ((rc = read_back(h, s, {status, status + 1}, bad))) return rc;
+    h->stats.nonspd_blocks = bad[0];
+    h->prepared = true;  // as the reference: the inverses exist (with the bad pivots in them)
+    if (bad[0] > 0) {
+        int level = 0;
+        for (int l = 1; l < h->L; ++l)
+            if (32 * bad[1] >= h->levelSize[2 * l + 1]) level = l;
+        return fail(h, MAS_ERR_NOT_SPD, std::to_string(bad[0]) + " block(s) met a zero, negative or non-finite "
+                    "pivot in LDL^T (first: block " + std::to_string(bad[1]) + ", level " + std::to_string(level) +
+                    "): the Hessian is not SPD there; the reference divides by it unchecked (.cpp:1406,1431)");
+    }
     return MAS_OK;
 }
 

@@ -26,7 +26,8 @@ FACADE_PATH = os.path.join(LIB_DIR, "libSeSchwarzPreconditioner.so")
 
 MAS_OK = 0
 STATUS = {0: "MAS_OK", -1: "MAS_ERR_ARG", -2: "MAS_ERR_HIP", -3: "MAS_ERR_CAPACITY", -4: "MAS_ERR_STATE",
-          -5: "MAS_ERR_LEVELS", -6: "MAS_ERR_NOMEM", -7: "MAS_ERR_NO_DEVICE", -8: "MAS_ERR_COMM"}
+          -5: "MAS_ERR_LEVELS", -6: "MAS_ERR_NOMEM", -7: "MAS_ERR_NO_DEVICE", -8: "MAS_ERR_COMM",
+          -9: "MAS_ERR_NOT_SPD"}
 
 # mas_allgather_fn(send, recv, bytes, stream, user) -> int
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
@@ -41,7 +42,7 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
            "mas_apply_shard_fine", "mas_apply_shard_complete", "mas_shard_apply_device", "mas_rccl_unique_id",
            "mas_rccl_init", "mas_shard_apply_rccl",
            "mas_pcg_solve_device", "mas_pcg_solve", "mas_blob_size", "mas_save_blob", "mas_load_blob",
-           "mas_blob_validate", "mas_dev_sort_pairs", "mas_dev_exclusive_scan"]
+           "mas_blob_validate", "mas_dev_sort_pairs", "mas_dev_exclusive_scan", "mas_dev_contact_terms"]
 
 
 class mas_config(ctypes.Structure):
@@ -64,7 +65,9 @@ class mas_stats(ctypes.Structure):
                [("apply_calls", ctypes.c_int64), ("profiled_applies", ctypes.c_int64)] + \
                [(n, ctypes.c_double) for n in ("apply_ms_avg", "pre_fine_ms_avg", "fine_ms_avg", "post_fine_ms_avg")] + \
                [("apply_mode", ctypes.c_int64), ("prepare_fine_ms", ctypes.c_double),
-                ("factor_formation", ctypes.c_int64), ("reserved", ctypes.c_int64 * 8)]
+                ("factor_formation", ctypes.c_int64), ("hier_dirty_level", ctypes.c_int64),
+                ("hier_rebuilt", ctypes.c_int64), ("prepare_fine_start_ms", ctypes.c_double),
+                ("nonspd_blocks", ctypes.c_int64), ("wait_timeouts", ctypes.c_int64), ("reserved", ctypes.c_int64 * 3)]
 
 
 class mas_shard(ctypes.Structure):
@@ -138,6 +141,7 @@ def lib():
         L.mas_shard_apply_rccl.argtypes = [P, P, P, P]
         L.mas_dev_sort_pairs.argtypes = [P, P, P, P, P, I, I, I]
         L.mas_dev_exclusive_scan.argtypes = [P, P, P, I, I]
+        L.mas_dev_contact_terms.argtypes = [P, P, P, P, P, I]
         F = ctypes.c_float
         L.mas_pcg_solve_device.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result), P]
         L.mas_pcg_solve.argtypes = [P, P, P, P, P, P, I, F, I, ctypes.POINTER(mas_pcg_result)]

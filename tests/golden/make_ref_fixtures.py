@@ -18,11 +18,16 @@ SeVector.h / SeCsr.h / SeAabb.h -- and records what that code computes:
   permutation (DoingSort, .cpp:238-243);
 * sizeof / alignof / offsetof of SeMatrix3f, Int2/Int4, Float2/3/4,
   SeMorton64 and SeCsr<int>, SeMatrix3f's element order, and SeCsr::Size /
-  IdxPtr on a sample CSR.
+  IdxPtr on a sample CSR;
+* (tests/golden/ref_contact.npz) the contact Hessian terms of
+  PrepareCollisionHessian / AdditionalSchwarzHessian2 (.cpp:1190,1208-1223)
+  evaluated with the reference's own Float3 / SeMatrix3f / OuterProduct /
+  Math::Square for the BASELINE contact stencils (VF of configs[2], the EF
+  and EE test records), random and edge directions, stiffnesses and weights.
 
 The outputs are data only (inputs and the reference code's outputs).
 
-Usage: python tests/golden/make_ref_fixtures.py
+Usage: python tests/golden/make_ref_fixtures.py [--contact-only]
 """
 from __future__ import annotations
 
@@ -99,6 +104,7 @@ def lib():
     L.refh_layout.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_longlong)]
     L.refh_csr_probe.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_void_p]
+    L.refh_contact_terms.argtypes = [ctypes.c_void_p, F, ctypes.c_void_p, ctypes.c_void_p]
     return L, so
 
 
@@ -118,8 +124,56 @@ def mesh_codes(L, pos):
     return codes, box
 
 
+def contact_inputs():
+    """(dir [N,3], stiff [N], w [N,5]) float32: the BASELINE stencils, random, edge."""
+    f = np.float32
+    one = f(1.0)
+    dirs, stiffs, ws = [], [], []
+    # configs[2] VF stencils (meshgen.vf_contacts: bary 0.25/0.25, normal z, stiff 100, zeroed
+    # records): weights -b0, -b1, -(1 - pad) (B-2, pad = 0), 1; and the fix_vf_bary form
+    for w2 in (-(one - f(0.0)), -(one - f(0.25) - f(0.25))):
+        dirs.append([0, 0, 1]); stiffs.append(100.0); ws.append([-0.25, -0.25, w2, 1.0, 0.0])
+    # meshgen.ef_contacts: bary (0.3, 0.2, 0.25), normal (0.6, 0, 0.8), stiff 50 (.cpp:326-354)
+    b0, b1, b2 = f(0.3), f(0.2), f(0.25)
+    dirs.append([0.6, 0.0, 0.8]); stiffs.append(50.0); ws.append([b0, one - b0, -b1, -b2, -((one - b1) - b2)])
+    # meshgen.ee_contacts: bary (0.4, 0.7), normal (0, 0.6, 0.8), stiff 80 (.cpp:355-380)
+    e0, e1 = f(0.4), f(0.7)
+    dirs.append([0.0, 0.6, 0.8]); stiffs.append(80.0); ws.append([e0, one - e0, -e1, -(one - e1), 0.0])
+    rng = np.random.default_rng(0xC0)
+    for _ in range(256):
+        d = rng.normal(size=3)
+        dirs.append(d / np.linalg.norm(d))
+        stiffs.append(10.0 ** rng.uniform(-2, 6))
+        ws.append(rng.uniform(-1, 1, size=5))
+    edge_w = [0.0, -0.0, 1.0, -1.0, 0.5, 1.0 / 3.0, 1e-20, -3e-39, 1e19, 2.0 ** -75, 7.0]
+    edge_d = [[0, 0, 0], [1, 0, 0], [-0.0, 1, 0], [1e-20, 1e-25, 1], [1e15, -1e15, 3e-39], [0.6, -0.8, 0.0]]
+    edge_s = [0.0, 1.0, 1e-30, 1e30, 3e-39, 100.0]
+    for i, d in enumerate(edge_d):
+        for j, st in enumerate(edge_s):
+            k = 5 * (i * len(edge_s) + j)
+            dirs.append(d); stiffs.append(st)
+            ws.append([edge_w[(k + q) % len(edge_w)] for q in range(5)])
+    return (np.asarray(dirs, f).reshape(-1, 3), np.asarray(stiffs, f), np.asarray(ws, f).reshape(-1, 5))
+
+
+def contact_fixtures(L):
+    dirs, stiffs, ws = contact_inputs()
+    out = np.zeros((dirs.shape[0], 234), np.float32)
+    for i in range(dirs.shape[0]):
+        d = np.ascontiguousarray(dirs[i])
+        w = np.ascontiguousarray(ws[i])
+        o = np.zeros(234, np.float32)
+        L.refh_contact_terms(P(d), float(stiffs[i]), P(w), P(o))
+        out[i] = o
+    np.savez_compressed(os.path.join(HERE, "ref_contact.npz"), dir=dirs, stiff=stiffs, w=ws, terms=out)
+    print(f"wrote tests/golden/ref_contact.npz ({dirs.shape[0]} stencils)")
+
+
 def main():
     L, so = lib()
+    contact_fixtures(L)
+    if "--contact-only" in sys.argv:
+        return
     out = {
         "generator": "tests/golden/make_ref_fixtures.py",
         "built_from": ["SeMorton.h", "SeMath.h", "SeMatrix.h", "SeVector.h", "SeCsr.h", "SeAabb.h",

@@ -25,6 +25,14 @@ def ref_arrays() -> dict:
         return {k: z[k] for k in z.files}
 
 
+@functools.lru_cache(maxsize=None)
+def ref_contact() -> dict:
+    """tests/golden/ref_contact.npz: dir [N,3], stiff [N], w [N,5] and the
+    reference headers' contact terms [N,234] (orc_contact_terms layout)."""
+    with np.load(os.path.join(GOLDEN, "ref_contact.npz")) as z:   # allow_pickle=False (default)
+        return {k: z[k] for k in z.files}
+
+
 def bits_to_f32(h: str) -> np.float32:
     return np.array([int(h, 16)], np.uint32).view(np.float32)[0]
 

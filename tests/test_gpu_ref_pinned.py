@@ -9,13 +9,19 @@ small parity meshes and a jittered 3-D cloud (tests/golden/make_ref_fixtures.py)
 Bar: bit-exact (hash of the whole array, a strided sample, full arrays for the
 small meshes); the reference's codes have no ties there, so the stable sort's
 permutation is the only valid one and is checked by hash too.
+
+The contact Hessian terms of the assembly kernels (k_assemble.hip
+contact_outer / contact_self / contact_pair / contact_double, through
+mas_dev_contact_terms) against tests/golden/ref_contact.npz -- what the
+reference's own Float3 / SeMatrix3f / OuterProduct / Math::Square compute for
+.cpp:1190,1208-1223.  Bar: bit-exact.
 """
 import ctypes
 
 import numpy as np
 import pytest
 
-from ref_fixtures import check_codes, mesh_positions, ref_json
+from ref_fixtures import check_codes, mesh_positions, ref_contact, ref_json
 
 pytestmark = pytest.mark.gpu
 
@@ -52,3 +58,17 @@ def test_gpu_morton_and_sort_match_reference(key):
     rc = P._L.mas_get_maps(P.h, _ptr(morton), _ptr(s2o), None, None, None, None, None)
     assert rc == 0, mas_amd.STATUS.get(rc, rc)
     check_codes(key, morton, s2o)
+
+
+def test_gpu_contact_terms_match_reference():
+    import mas_amd
+    from mas_amd import _ptr
+    c = ref_contact()
+    n = c["dir"].shape[0]
+    P = mas_amd.SeSchwarzPreconditioner()
+    out = np.zeros((n, 234), np.float32)
+    args = [np.ascontiguousarray(c[k], np.float32) for k in ("dir", "stiff", "w")]
+    rc = P._L.mas_dev_contact_terms(P.h, *[_ptr(a) for a in args], _ptr(out), n)
+    assert rc == 0, mas_amd.STATUS.get(rc, rc)
+    bad = np.argwhere(out.view(np.uint32) != c["terms"].view(np.uint32))
+    assert bad.size == 0, f"{len(bad)} terms differ, first stencil {bad[0][0]} entry {bad[0][1]}"
