@@ -44,9 +44,9 @@ extern "C" {
  *    first_pass_iterations, replacements) and gained a reserved tail, so later
  *    additions do not change their size again; mas_config.reference_formation;
  *    MAS_ERR_COMM. */
-/* 3: MAS_ERR_NOT_SPD; mas_stats' reserved tail now carries hier_dirty_level,
- *    hier_rebuilt, prepare_fine_start_ms, nonspd_blocks, wait_timeouts (same
- *    size). */
+/* 3: MAS_ERR_NOT_SPD; mas_config.reference_restriction; mas_stats' reserved
+ *    tail now carries hier_dirty_level, hier_rebuilt, prepare_fine_start_ms,
+ *    nonspd_blocks, wait_timeouts (same sizes). */
 #define MAS_ABI_VERSION 3
 
 typedef enum {
@@ -80,7 +80,14 @@ typedef struct {
                                 1 = the reference's own operation order on the vector ALUs
                                 (.cpp:1437-1495): every inverse bitwise equal to the reference
                                 arithmetic, ~0.15 ms more Prepare at 1M */
-    int reserved[10];
+    int reference_restriction; /* ABI 3.  0 = the level-3 residual is the sum of its children's level-2
+                                  residuals in level-2 id order (default: a 32-add chain; R1 and R2 stay
+                                  bitwise the reference's, R3 is the same sum associated by level-2
+                                  node, z within 1e-5); 1 = the reference's own association
+                                  (BuildResidualHierarchy .cpp:1581-1590: every R1 folded into R3 in
+                                  level-1 id order, a 1 024-add chain at 1M): the whole residual
+                                  hierarchy bitwise the reference arithmetic, ~6 us more per apply */
+    int reserved[9];
 } mas_config;
 
 typedef struct {
@@ -312,7 +319,8 @@ int mas_get_block_inverse(mas_handle h, int blk, float* out96x96);
  * over coarse node ids begin_1 .. total_clusters-1.  Only levels
  * 1 .. min(L-1, 3) are computed: at L = 5 the level-4 entries are 0 (that
  * level is never prolonged, CollectFinalZ .cpp:1706-1717, so it is skipped),
- * where the reference's m_mappedR holds the sums. */
+ * where the reference's m_mappedR holds the sums.  Level 3 is the sum of the
+ * level-2 residuals unless mas_config.reference_restriction = 1. */
 int mas_get_coarse_residual(mas_handle h, float* out4);
 /* Diagnostics of Prepare's building blocks on device buffers (tests): the
  * stable pair sort by the low `bits` key bits and the int exclusive scan, on

@@ -300,7 +300,9 @@ void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStre
     float4* rc = P<float4>(h->Rc);
     float4* zc = P<float4>(h->Zc);
     const int begin1 = h->levelSize[3];
-    for (int l = lFirst; l < h->L && l < 3; ++l) {
+    // grouped level 3 (the default): R3 from R2 like level 2 from R1; else the reference's fold over R1
+    const int lTop = h->groupedR3 ? 4 : 3;
+    for (int l = lFirst; l < h->L && l < lTop; ++l) {
         const int cnt = h->levelSize[2 * l], beg = h->levelSize[2 * l + 1];
         const int nb = ceil32(cnt) / 32;
         if (l == 1)
@@ -311,7 +313,7 @@ void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStre
                                                                       h->levelSize[2 * (l - 1) + 1], rc, zc, begin1,
                                                                       h->applyDone);
     }
-    if (h->L >= 4) launch_coarse_deep(h, nullptr, nullptr, s);
+    if (h->L >= 4 && !h->groupedR3) launch_coarse_deep(h, nullptr, nullptr, s);
 }
 
 // z[s2o[v]] += Z1[a1]; += Z2[a2]; += Z3[a3] for v in [v0, v1) -- the
@@ -362,7 +364,12 @@ void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float
 // tagged form at L = 3 (256k: 34.3 -> 32.3 us per apply) and the two-launch
 // form at L >= 4, where the one-launch form measured from 2 us faster to 6 us
 // slower at 1M depending on the box
-int coarse_mode(const mas_context* h) { return h->coarseMode >= 0 ? h->coarseMode : (h->L == 3 ? 3 : 2); }
+// (the one-launch form folds level 3 in the reference's order only: with the
+// grouped level 3 at L >= 4 an apply runs the two-launch form instead)
+int coarse_mode(const mas_context* h) {
+    const int m = h->coarseMode >= 0 ? h->coarseMode : (h->L == 3 ? 3 : 2);
+    return m == 3 && h->groupedR3 && h->L >= 4 ? 2 : m;
+}
 
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     if (h->L >= 4 && !h->deepOff.p) return fail(h, MAS_ERR_STATE, "apply: deep-level lists not built");

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_restrict12(int n1, int begin1, i
     const int c = c0 + j;
     const bool own = lane < 32 && c < n1;
     const int parent = own && L >= 3 ? goingNext[begin1 + c] - begin1 : 0;
-    const int dpos = own && L >= 4 ? deepPos[c] : -1;
+    const int dpos = own && L >= 4 && deepPos ? deepPos[c] : -1;  // null: grouped level 3, no lists
     float4 val[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) val[q] = src[q] >= 0 ? r[src[q]] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -232,6 +232,74 @@ __global__ __launch_bounds__(THREADS) void k_solve123(const float4* __restrict__
     // (sleep 32 / 64 / 127: 19.9 / 19.4 / 19.9 us).
     if (q.nDeepNodes > 0) __builtin_amdgcn_s_sleep(64);
     const int w = (blockIdx.x - q.nDeepNodes) * (THREADS / 64) + (threadIdx.x >> 6);
+    if (w >= q.nb1 + q.nb2) return;  // wave-uniform
+    solve12_wave(inv, rc, zc, q, w);
+}
+
+// Grouped level 3 (mas_config.reference_restriction = 0, the default).  R3 of
+// a level-3 node = its children's R2 -- the lanes of one component of one
+// level-2 bank (members) -- folded in level-2 id order from +0, R2 from
+// k_restrict12: a 32-add chain per node instead of the reference's 1 024-add
+// fold over R1 (deep_fold.h), the same sum associated by level-2 node.  One
+// wave per level-3 block: the 1 024 child slots of its 32 nodes are gathered
+// 16 per lane (item 64 q + lane = node 2 q + lane / 32, child lane % 32;
+// masked-out children +0.0, exact in a fold from +0) into LDS, lane n folds
+// node n's row, then Z3 = Inv R3 with the inverse loaded at wave start.
+struct Solve3 {
+    int b3, nb3, n3;       // level-3 blocks [b3, b3 + nb3), n3 nodes
+    int lv3Begin, lv2Begin;
+};
+
+__device__ __forceinline__ void solve3_grouped_wave(const float4* __restrict__ inv, const int2* __restrict__ members,
+                                                    float4* __restrict__ rc, float4* __restrict__ zc, int begin1,
+                                                    const Solve3& q3, int k, float (&sv)[3][32][33]) {
+    const int lane = threadIdx.x & 63, n = lane & 31, j = lane & 31;
+    const int blk = q3.b3 + k, node = blk * 32 + n;
+    const bool own = lane < 32 && node - q3.lv3Begin < q3.n3;
+    float g[kRecord], tl[3];
+    load_record<true>(inv, blk, lane, g, tl);
+    const int2 mb = own ? members[node - begin1] : make_int2(0, 0);
+    const int base = q3.lv2Begin - begin1;  // Rc index of level-2 local id 0
+    float4 v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int nn = 2 * q + (lane >> 5);
+        const int bank = __shfl(mb.x, nn);
+        const unsigned msk = (unsigned)__shfl(mb.y, nn);
+        v[q] = (msk >> j) & 1u ? rc[base + bank * 32 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        sv[0][2 * q + (lane >> 5)][j] = v[q].x;
+        sv[1][2 * q + (lane >> 5)][j] = v[q].y;
+        sv[2][2 * q + (lane >> 5)][j] = v[q].z;
+    }
+    __builtin_amdgcn_wave_barrier();
+    float3 a = make_float3(0.f, 0.f, 0.f);
+    if (own) a = fold32_soa(sv[0][n], sv[1][n], sv[2][n]);
+    const float ax = __shfl(a.x, n), ay = __shfl(a.y, n), az = __shfl(a.z, n);  // half 1 takes node n's R
+    const float3 out = block_solve(g, tl, make_float3(ax, ay, az), lane);
+    if (lane < 32) {
+        rc[node - begin1] = make_float4(ax, ay, az, 0.f);
+        zc[node - begin1] = make_float4(out.x, out.y, out.z, 0.f);
+    }
+}
+
+// Grouped form of k_solve123: workgroups [0, nb3) give their wave 0 to a
+// level-3 block (LDS for one), every other wave solves a level-1/2 block.
+// Nothing waits on anything inside the launch.
+__global__ __launch_bounds__(kApplyThreads) void k_solve123g(const float4* __restrict__ inv,
+                                                            const int2* __restrict__ members,
+                                                            float4* __restrict__ rc, float4* __restrict__ zc,
+                                                            Solve12 q, Solve3 q3, const int* __restrict__ done) {
+    if (done && *done) return;
+    __shared__ float sv[3][32][33];
+    const int wv = threadIdx.x >> 6, g = blockIdx.x;
+    if (g < q3.nb3 && wv == 0) {  // wave-uniform
+        solve3_grouped_wave(inv, members, rc, zc, q.begin1, q3, g, sv);
+        return;
+    }
+    const int w = g * (kApplyThreads / 64) + wv - min(q3.nb3, g + 1);
     if (w >= q.nb1 + q.nb2) return;  // wave-uniform
     solve12_wave(inv, rc, zc, q, w);
 }
@@ -319,17 +387,19 @@ void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
     // 11.3 us; at 1M the restriction alone this way measured no gain)
     const bool narrow = h->coarseNarrow > 0 || (h->coarseNarrow < 0 && h->L == 3);
     const dim3 rg(cdiv(nb1, kRestrictWaves)), rb(64 * kRestrictWaves);
+    const bool grouped = h->groupedR3 && h->L >= 4;
+    const int* deepPos = grouped ? nullptr : P<int>(h->deepPos);  // grouped: no level-3 lists to fill
     if (narrow && !occ)
         k_restrict12<false, 1><<<nb1, 64, 0, s>>>(n1, begin1, h->L, P<int>(h->l1src), P<int>(h->goingNext),
-                                                  P<int2>(h->members), r, P<float4>(h->Rc), P<int>(h->deepPos),
+                                                  P<int2>(h->members), r, P<float4>(h->Rc), deepPos,
                                                   P<float4>(h->deepR1), h->applyDone);
     else if (occ)
         k_restrict12<true><<<rg, rb, 0, s>>>(n1, begin1, h->L, P<int>(h->l1src), P<int>(h->goingNext),
-                                             P<int2>(h->members), r, P<float4>(h->Rc), P<int>(h->deepPos),
+                                             P<int2>(h->members), r, P<float4>(h->Rc), deepPos,
                                              P<float4>(h->deepR1), h->applyDone);
     else
         k_restrict12<false><<<rg, rb, 0, s>>>(n1, begin1, h->L, P<int>(h->l1src), P<int>(h->goingNext),
-                                              P<int2>(h->members), r, P<float4>(h->Rc), P<int>(h->deepPos),
+                                              P<int2>(h->members), r, P<float4>(h->Rc), deepPos,
                                               P<float4>(h->deepR1), h->applyDone);
     Solve12 q{};
     q.begin1 = begin1;
@@ -341,6 +411,18 @@ void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s) {
     q.n2 = h->levelSize[4];
     q.b2 = q.lv2Begin / 32;
     q.nb2 = ceil32(q.n2) / 32;
+    if (grouped) {
+        Solve3 q3{};
+        q3.n3 = h->levelSize[6];
+        q3.lv3Begin = h->levelSize[7];
+        q3.lv2Begin = q.lv2Begin;
+        q3.b3 = q3.lv3Begin / 32;
+        q3.nb3 = ceil32(q3.n3) / 32;
+        const int grid = std::max(q3.nb3, cdiv(q3.nb3 + q.nb1 + q.nb2, kApplyThreads / 64));
+        k_solve123g<<<grid, kApplyThreads, 0, s>>>(P<float4>(h->inv), P<int2>(h->members), P<float4>(h->Rc),
+                                                   P<float4>(h->Zc), q, q3, h->applyDone);
+        return;
+    }
     const DeepArgs d = deep_args(h, P<float4>(h->deepR1), nullptr);
     q.nDeepNodes = deep_nodes(h);
     const dim3 sg(q.nDeepNodes + cdiv(q.nb1 + q.nb2, kApplyThreads / 64));

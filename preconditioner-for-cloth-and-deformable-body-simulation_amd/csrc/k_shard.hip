@@ -83,6 +83,79 @@ __global__ __launch_bounds__(256) void k_shard_pos1(int n1, int world, int segMa
     pos1[i] = lo * segMax + (i - off[lo]);
 }
 
+// Grouped level 3 of a sharded apply (mas_config.reference_restriction = 0):
+// node T's children are the lanes of one component of one level-2 bank
+// (members); lane j computes child j's R2 from the gathered R1 exactly as the
+// level-2 waves below (its children in lane order from +0), then R3 is those
+// R2 folded in lane order from +0 -- bitwise the unsharded grouped level 3
+// (k_coarse.hip solve3_grouped_wave over k_restrict12's R2).  Wave 0 computes
+// and publishes R3 and counts the arrival; the block's last arriver solves
+// the block with the inverse wave 1 prefetched (deep_fold.h protocol).
+__device__ __forceinline__ void deep_node_grouped(const float4* __restrict__ inv, int node,
+                                                  const float4* __restrict__ gathered, const int* __restrict__ pos1,
+                                                  const int2* __restrict__ members, int lv2Begin, int begin1,
+                                                  float4* __restrict__ rc, float4* __restrict__ zc, const DeepArgs& d) {
+    __shared__ int last;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, j = lane & 31;
+    const int blk = node >> 5;
+    float g[kRecord], tl[3];
+    if (w == 1) load_record<true>(inv, blk, lane, g, tl);
+    if (w == 0) {
+        const int2 mbT = members[node - begin1];  // (level-2 bank, children)
+        const bool child = lane < 32 && (((unsigned)mbT.y >> j) & 1u);
+        float ax = 0.f, ay = 0.f, az = 0.f;
+        if (child) {
+            const int2 mb = members[lv2Begin + mbT.x * 32 + j - begin1];  // (level-1 bank, children)
+            const unsigned msk = (unsigned)mb.y;
+            const int4* p4 = reinterpret_cast<const int4*>(pos1 + mb.x * 32);
+            int src[32];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int4 v = p4[q];
+                src[4 * q] = v.x;
+                src[4 * q + 1] = v.y;
+                src[4 * q + 2] = v.z;
+                src[4 * q + 3] = v.w;
+            }
+            float vx[32], vy[32], vz[32];
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                const float4 v = gathered[(msk >> k) & 1u ? src[k] : 0];
+                vx[k] = v.x; vy[k] = v.y; vz[k] = v.z;
+            }
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+                if ((msk >> k) & 1u) {
+                    ax = __fadd_rn(ax, vx[k]);
+                    ay = __fadd_rn(ay, vy[k]);
+                    az = __fadd_rn(az, vz[k]);
+                }
+        }
+        // R3: the children's R2 in lane order from +0 (others +0.0)
+        float bx = 0.f, by = 0.f, bz = 0.f;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            bx = __fadd_rn(bx, __shfl(ax, k));
+            by = __fadd_rn(by, __shfl(ay, k));
+            bz = __fadd_rn(bz, __shfl(az, k));
+        }
+        if (t == 0) {
+            st_wt(rc + node - begin1, make_float4(bx, by, bz, 0.f));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int old = __hip_atomic_fetch_add(d.cnt + (blk - d.lv3Begin / 32), 1, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+            last = old == 31;
+        }
+    }
+    __syncthreads();
+    if (!last || w != 1) return;
+    if (lane == 0) d.cnt[blk - d.lv3Begin / 32] = 0;  // for the next apply (visible after this kernel)
+    const int n = lane & 31;
+    const float4 R = ld_wt(rc + blk * 32 + n - begin1);
+    const float3 out = block_solve(g, tl, make_float3(R.x, R.y, R.z), lane);
+    if (lane < 32) zc[blk * 32 + n - begin1] = make_float4(out.x, out.y, out.z, 0.f);
+}
+
 // Levels 1 and 2 of a sharded apply in ONE launch, straight from the gathered
 // segments (no unpack pass): waves [0, nOwn1) solve the rank's own level-1
 // blocks (Z1 = Inv R1), waves [nOwn1, nOwn1 + nb2) compute R2 of every level-2
@@ -95,9 +168,13 @@ __global__ __launch_bounds__(256) void k_shard_pos1(int n1, int world, int segMa
 __global__ __launch_bounds__(kApplyThreads) void k_shard_coarse12(
     const float4* __restrict__ inv, const float4* __restrict__ gathered, const int* __restrict__ pos1, int own1Blk0,
     int nOwn1, int n1, int lv2Blk0, int nb2, int n2, const int2* __restrict__ members, int begin1,
-    float4* __restrict__ rc, float4* __restrict__ zc, DeepArgs d, int nDeep) {
+    float4* __restrict__ rc, float4* __restrict__ zc, DeepArgs d, int nDeep, int groupedLv2Begin) {
     if ((int)blockIdx.x < nDeep) {  // workgroup-uniform
-        deep_node<true>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, begin1);
+        if (groupedLv2Begin >= 0)
+            deep_node_grouped(inv, d.lv3Begin + blockIdx.x, gathered, pos1, members, groupedLv2Begin, begin1, rc, zc,
+                              d);
+        else
+            deep_node<true>(inv, d.lv3Begin + blockIdx.x, d, rc, zc, begin1);
         return;
     }
     // the level-1/2 waves have slack: held back as in k_solve123 (one-rank
@@ -249,13 +326,15 @@ static int shard_coarse(mas_context* h, const mas_shard& sh, int world, const fl
     const int nb2 = h->L > 2 ? ceil32(h->levelSize[4]) / 32 : 0;
     const int n2 = h->L > 2 ? h->levelSize[4] : 0;
     const int lv2Blk0 = h->L > 2 ? h->levelSize[5] / 32 : 0;
-    // level 3 in the same launch: R folded from the gathered R1 in the reference's order
+    // level 3 in the same launch: R from the gathered R1, grouped by level-2
+    // node (the default) or folded in the reference's order
     const DeepArgs d = deep_args(h, reinterpret_cast<const float4*>(d_gathered4), P<int>(h->deepIdxShard));
     const int nDeep = deep_nodes(h);
     if (nDeep + nOwn1 + nb2 > 0)
         k_shard_coarse12<<<nDeep + cdiv(nOwn1 + nb2, kApplyThreads / 64), kApplyThreads, 0, s>>>(
             P<float4>(h->inv), reinterpret_cast<const float4*>(d_gathered4), P<int>(h->shardPos1), begin1 / 32 + own0,
-            nOwn1, n1, lv2Blk0, nb2, n2, P<int2>(h->members), begin1, P<float4>(h->Rc), P<float4>(h->Zc), d, nDeep);
+            nOwn1, n1, lv2Blk0, nb2, n2, P<int2>(h->members), begin1, P<float4>(h->Rc), P<float4>(h->Zc), d, nDeep,
+            h->groupedR3 ? h->levelSize[5] : -1);
     return MAS_OK;
 }
 

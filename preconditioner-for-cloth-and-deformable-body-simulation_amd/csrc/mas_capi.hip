@@ -183,6 +183,8 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_COARSE_WIDE")) h->coarseWide = std::atoi(v);
     if (const char* v = std::getenv("MAS_SORT")) h->sortImpl = std::atoi(v);
     if (h->cfg.reference_formation) h->factorVariant = 4;
+    h->groupedR3 = !h->cfg.reference_restriction;
+    if (const char* v = std::getenv("MAS_REF_RESTRICT")) h->groupedR3 = !std::atoi(v);
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_POLL_DELAY")) h->c1PollDelay = std::atoi(v);

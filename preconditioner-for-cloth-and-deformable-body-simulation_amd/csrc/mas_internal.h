@@ -122,6 +122,10 @@ struct mas_context {
     // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (The
     // side-stream overlap was measured slower: DESIGN.md section 4.)
     int coarseMode = -1;  // -1: 3 at L = 3, 2 at L >= 4 (measured)
+    // level-3 residual (mas_config.reference_restriction, env MAS_REF_RESTRICT):
+    // true = the sum of its children's R2 (default), false = the reference's
+    // fold of every R1 in level-1 id order (deep_fold.h)
+    bool groupedR3 = true;
     // coarse launches in their occupancy forms (k_coarse.hip): -1 = when the
     // level-1 level has >= kCoarseOccBlocks blocks, 0 = never, 1 = always;
     // env MAS_COARSE_OCC

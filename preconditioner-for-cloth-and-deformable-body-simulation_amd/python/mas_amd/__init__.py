@@ -48,7 +48,8 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
 class mas_config(ctypes.Structure):
     _fields_ = [("max_levels", ctypes.c_int), ("resort_period", ctypes.c_int), ("fix_vf_bary", ctypes.c_int),
                 ("device", ctypes.c_int), ("keep_blocks", ctypes.c_int),
-                ("reference_formation", ctypes.c_int), ("reserved", ctypes.c_int * 10)]
+                ("reference_formation", ctypes.c_int), ("reference_restriction", ctypes.c_int),
+                ("reserved", ctypes.c_int * 9)]
 
 
 class mas_info(ctypes.Structure):
@@ -205,10 +206,10 @@ class SeSchwarzPreconditioner:
     """Reference-compatible surface (SE::SeSchwarzPreconditioner) on the GPU."""
 
     def __init__(self, max_levels: int = 0, resort_period: int = 0, fix_vf_bary: bool = False, device: int = -1,
-                 keep_blocks: bool = False, reference_formation: bool = False):
+                 keep_blocks: bool = False, reference_formation: bool = False, reference_restriction: bool = False):
         self._L = lib()
         cfg = mas_config(max_levels, resort_period, int(fix_vf_bary), device, int(bool(keep_blocks)),
-                         int(bool(reference_formation)))
+                         int(bool(reference_formation)), int(bool(reference_restriction)))
         h = ctypes.c_void_p()
         rc = self._L.mas_create(ctypes.byref(h), ctypes.byref(cfg))
         if rc != MAS_OK:

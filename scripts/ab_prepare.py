@@ -21,7 +21,8 @@ for v in args.variants:
     for k, old in saved.items():
         if old is None: os.environ.pop(k)
         else: os.environ[k] = old
-keys = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms")
+keys = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms", "prepare_fine_ms",
+        "prepare_fine_start_ms")
 res = {v: {k: [] for k in keys} for v in args.variants}
 for rnd in range(args.rounds):
     for v in args.variants:

@@ -22,5 +22,5 @@ for _ in range(reps):
         P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, contacts[0], None, None, contacts[1])
     st = P.stats()
     print(f"prepare {st['prepare_ms']:.3f} ms (levels {st['prepare_levels_ms']:.3f}, assemble "
-          f"{st['prepare_assemble_ms']:.3f}, factor {st['prepare_factor_ms']:.3f}, fused level-0 {st['prepare_fine_ms']:.3f}); host {1e3*(time.perf_counter()-t0):.1f} ms",
+          f"{st['prepare_assemble_ms']:.3f}, factor {st['prepare_factor_ms']:.3f}, fused level-0 {st['prepare_fine_ms']:.3f} from {st['prepare_fine_start_ms']:.3f}, hier rebuilt {st['hier_rebuilt']}); host {1e3*(time.perf_counter()-t0):.1f} ms",
           flush=True)

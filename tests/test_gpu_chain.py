@@ -5,7 +5,10 @@
 Every sum runs in the same order in both forms, so the bar is BITWISE
 equality, per apply, over many back-to-back applies with a different residual
 each time (a stale coarse value would show up as a mismatch in some later
-apply), and the oracle bar (1e-5) for the result itself.
+apply), and the oracle bar (1e-5) for the result itself.  With the
+reference's level-3 order (mas_config.reference_restriction = 1) all five
+forms run; with the default grouped level 3 the per-level and two-launch
+forms (the one-launch form hands level 3 to the two-launch form at L >= 4).
 """
 import numpy as np
 import pytest
@@ -15,7 +18,7 @@ from conftest import cloth, tet
 pytestmark = pytest.mark.gpu
 
 
-def _handles(mesh, L, contacts, monkeypatch):
+def _handles(mesh, L, contacts, monkeypatch, grouped=False):
     """Per-level (mode 0), two-pass (2), two-pass in its occupancy form
     (SoA restriction staging, no level-3 inverse prefetch) and one-launch (3)
     handles."""
@@ -25,8 +28,9 @@ def _handles(mesh, L, contacts, monkeypatch):
         monkeypatch.setenv("MAS_COARSE_MODE", str(mode))
         monkeypatch.setenv("MAS_COARSE_OCC", str(occ))
         monkeypatch.setenv("MAS_COARSE_WIDE", str(wide))
-        hs.append(mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts))
-        assert hs[-1].stats()["apply_mode"] == mode
+        hs.append(mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, reference_restriction=not grouped))
+        nL = hs[-1].info()["num_levels"]
+        assert hs[-1].stats()["apply_mode"] == (2 if mode == 3 and grouped and nL >= 4 else mode)
     return hs
 
 
@@ -46,12 +50,13 @@ CASES = [("cloth", 20, 0, 0), ("cloth", 40, 2, 0), ("cloth", 100, 3, 0), ("cloth
 
 
 @pytest.mark.parametrize("kind,W,L,nc", CASES)
-def test_twopass_equals_per_level(kind, W, L, nc, monkeypatch):
+@pytest.mark.parametrize("grouped", [False, True])
+def test_twopass_equals_per_level(kind, W, L, nc, grouped, monkeypatch):
     import torch
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=11) if nc else None
-    P3, P2, P2o, P1, P2w = _handles(mesh, L, contacts, monkeypatch)
+    P3, P2, P2o, P1, P2w = _handles(mesh, L, contacts, monkeypatch, grouped)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 100 + k)).cuda() for k in range(24)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
@@ -65,7 +70,8 @@ def test_twopass_equals_per_level(kind, W, L, nc, monkeypatch):
             np.testing.assert_array_equal(a, b, err_msg=f"second pass, apply {k}")
 
 
-def test_twopass_1m_contacts_bitwise_and_oracle(monkeypatch):
+@pytest.mark.parametrize("grouped", [False, True])
+def test_twopass_1m_contacts_bitwise_and_oracle(grouped, monkeypatch):
     """The bench workload: 1M cloth + 100k VF contacts, 4 levels; two-pass =
     per-level bitwise over 40 back-to-back applies, and the oracle bar."""
     import torch
@@ -73,7 +79,7 @@ def test_twopass_1m_contacts_bitwise_and_oracle(monkeypatch):
     from oracle import Oracle
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    P3, P2, P2o, P1, P2w = _handles(mesh, 4, contacts, monkeypatch)
+    P3, P2, P2o, P1, P2w = _handles(mesh, 4, contacts, monkeypatch, grouped)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 0x5EED + k)).cuda() for k in range(40)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)

@@ -8,7 +8,12 @@ a sum of the level-(l-1) R.  The GPU follows that order (k_restrict12 for
 levels 1-2, the deep folds of k_coarse_twopass.hip for levels >= 3), so R of
 every real coarse node of the prolonged levels (1..3; level 4 never reaches
 z, B-6, and is not computed) equals the oracle's m_mappedR bit for bit, in
-both coarse launch forms.
+every coarse launch form -- with mas_config.reference_restriction = 1.
+
+The default (grouped) level 3 is the sum of the level-2 residuals instead
+(another association of the same sum): there R1 and R2 are still the
+oracle's bit for bit, and R3 is checked bit for bit against an fp32 left fold
+of the oracle's R2 over each level-3 node's children in level-2 id order.
 """
 import numpy as np
 import pytest
@@ -26,7 +31,19 @@ def _real_nodes(ls, L):
     return [(int(flat[2 * l + 1]), int(flat[2 * l])) for l in range(1, min(L, 4))]
 
 
-def _check(P, o, r, tag=""):
+def _grouped_r3(Ro, gn, ls):
+    """Level-3 R as the grouped form computes it: each node's children's R2
+    (level-2 ids ascending) folded left in fp32 from +0."""
+    flat = ls.reshape(-1)
+    b2, n2, b3, n3 = int(flat[5]), int(flat[4]), int(flat[7]), int(flat[6])
+    acc = np.zeros((n3, 3), np.float32)
+    for c in range(b2, b2 + n2):
+        t = int(gn[c]) - b3
+        acc[t] = (acc[t] + Ro[c, :3]).astype(np.float32)
+    return acc
+
+
+def _check(P, o, r, tag="", grouped=False):
     import torch
     rd = torch.from_numpy(r).cuda()
     zd = torch.zeros_like(rd)
@@ -43,6 +60,8 @@ def _check(P, o, r, tag=""):
     for lv, (b, n) in enumerate(_real_nodes(ls, L), start=1):
         g = Rg[b - begin1:b - begin1 + n, :3]
         e = Ro[b:b + n, :3]
+        if lv == 3 and grouped:
+            e = _grouped_r3(Ro, o.maps()["going_next"], ls)
         bad = np.flatnonzero(np.any(g.view(np.uint32) != e.view(np.uint32), axis=1))
         assert bad.size == 0, (tag, lv, n, bad[:5], g[bad[:3]], e[bad[:3]])
 
@@ -50,14 +69,15 @@ def _check(P, o, r, tag=""):
 @pytest.mark.parametrize("kind,W,L,nc", [("cloth", 100, 4, 0), ("cloth", 256, 4, 2000), ("cloth", 512, 5, 0),
                                          ("tet", 16, 4, 0), ("cloth", 64, 3, 0)])
 @pytest.mark.parametrize("mode", [0, 2, 3])
-def test_residual_hierarchy_bitwise(kind, W, L, nc, mode, monkeypatch):
+@pytest.mark.parametrize("grouped", [False, True])
+def test_residual_hierarchy_bitwise(kind, W, L, nc, mode, grouped, monkeypatch):
     import mas_amd
     from mas_amd import meshgen
     from oracle import Oracle
     monkeypatch.setenv("MAS_COARSE_MODE", str(mode))
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=5) if nc else None
-    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
+    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, reference_restriction=not grouped)
     o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], L, 8)
     o.allocate(mesh)
     if contacts is not None:
@@ -65,10 +85,11 @@ def test_residual_hierarchy_bitwise(kind, W, L, nc, mode, monkeypatch):
     else:
         o.prepare(mesh)
     for k in range(3):
-        _check(P, o, meshgen.residual(mesh.nV, 40 + k), f"apply {k}")
+        _check(P, o, meshgen.residual(mesh.nV, 40 + k), f"apply {k}", grouped)
 
 
-def test_residual_hierarchy_1m_contacts():
+@pytest.mark.parametrize("grouped", [False, True])
+def test_residual_hierarchy_1m_contacts(grouped):
     """The bench workload (1M cloth + 100k VF contacts, 4 levels): the level-3
     nodes each fold ~1 000 level-1 values."""
     import mas_amd
@@ -76,14 +97,15 @@ def test_residual_hierarchy_1m_contacts():
     from oracle import Oracle
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    P = mas_amd.from_mesh(mesh, max_levels=4, contacts=contacts)
+    P = mas_amd.from_mesh(mesh, max_levels=4, contacts=contacts, reference_restriction=not grouped)
     o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], 4, 8)
     o.allocate(mesh)
     o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
-    _check(P, o, meshgen.residual(mesh.nV, 0x5EED))
+    _check(P, o, meshgen.residual(mesh.nV, 0x5EED), grouped=grouped)
 
 
-def test_level3_handoff_across_xcds_4m_tet():
+@pytest.mark.parametrize("grouped", [False, True])
+def test_level3_handoff_across_xcds_4m_tet(grouped):
     """The level-3 hand-off between workgroups (deep_fold.h: each node's R
     published with write-through agent-scope stores, drained, then an
     agent-scope arrival count; the block's last node reads the others' R with
@@ -98,7 +120,7 @@ def test_level3_handoff_across_xcds_4m_tet():
     from mas_amd import meshgen
     from oracle import Oracle
     mesh, cfg = meshgen.build_config("4M-tet")
-    P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"])
+    P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], reference_restriction=not grouped)
     inf = P.info()
     assert int(inf["level_size"][3][0]) == 574
     o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], cfg["levels"], 16)
@@ -107,9 +129,9 @@ def test_level3_handoff_across_xcds_4m_tet():
     r_rand = meshgen.residual(mesh.nV, 77)
     r_smooth = np.zeros_like(r_rand)
     r_smooth[:, :3] = 1.0
-    _check(P, o, r_rand, "random")
-    _check(P, o, r_smooth, "smooth")          # P's previous apply had r_rand
-    Q = mas_amd.from_mesh(mesh, max_levels=cfg["levels"])
+    _check(P, o, r_rand, "random", grouped)
+    _check(P, o, r_smooth, "smooth", grouped)          # P's previous apply had r_rand
+    Q = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], reference_restriction=not grouped)
     z = []
     for H in (P, Q):
         rd = torch.from_numpy(r_smooth).cuda()

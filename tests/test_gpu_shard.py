@@ -49,15 +49,18 @@ def _unsharded(P, r):
 @pytest.mark.parametrize("kind,W,L,worlds,nc", [("cloth", 64, 0, (1, 2, 3, 8), 0), ("cloth", 100, 1, (2, 5), 0),
                                                 ("tet", 16, 3, (2, 4), 0), ("cloth", 1024, 4, (2, 8), 0),
                                                 ("cloth", 1024, 4, (8,), 100_000), ("tet", 160, 4, (8,), 0)])
-def test_virtual_shards_bitwise(kind, W, L, worlds, nc):
+@pytest.mark.parametrize("grouped", [True, False])
+def test_virtual_shards_bitwise(kind, W, L, worlds, nc, grouped):
     """Includes BASELINE configs[3] (1M + 100k VF contacts, 8 ranks) and
-    configs[4] (4M tet lattice, 8 ranks: ~26k level-1 nodes per rank)."""
+    configs[4] (4M tet lattice, 8 ranks: ~26k level-1 nodes per rank); both
+    level-3 forms (grouped: R3 from the children's R2 recomputed in the
+    level-3 workgroups; reference: the fold over every gathered R1)."""
     import torch
     import mas_amd
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=3) if nc else None
-    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
+    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, reference_restriction=not grouped)
     r = torch.from_numpy(meshgen.residual(mesh.nV, 3)).cuda()
     z_ref = torch.zeros_like(r)
     torch.cuda.synchronize()
