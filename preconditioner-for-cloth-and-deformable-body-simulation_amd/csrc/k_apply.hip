@@ -361,14 +361,16 @@ void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float
 }
 
 // the coarse form an apply uses: the env / config choice, else the one-launch
-// tagged form at L = 3 (256k: 34.3 -> 32.3 us per apply) and the two-launch
-// form at L >= 4, where the one-launch form measured from 2 us faster to 6 us
-// slower at 1M depending on the box
-// (the one-launch form folds level 3 in the reference's order only: with the
-// grouped level 3 at L >= 4 an apply runs the two-launch form instead)
+// tagged form at L = 3 (256k: 34.3 -> 32.3 us per apply) and at L >= 4 with
+// the grouped level 3.
+// With the grouped level 3 (the default) the one-launch form wins at L >= 4
+// too (1M + contacts: pre-fine 17.9 -> 14.7 us, 4M tet 50.1 -> 47.5 us,
+// profiles/round4/apply/); with the reference's 1 024-add level-3 fold it
+// measured from 2 us faster to 6 us slower at 1M (round 3), so that mode
+// keeps the two-launch form at L >= 4.
 int coarse_mode(const mas_context* h) {
-    const int m = h->coarseMode >= 0 ? h->coarseMode : (h->L == 3 ? 3 : 2);
-    return m == 3 && h->groupedR3 && h->L >= 4 ? 2 : m;
+    if (h->coarseMode >= 0) return h->coarseMode;
+    return h->L == 3 || (h->L >= 4 && h->groupedR3) ? 3 : 2;
 }
 
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {

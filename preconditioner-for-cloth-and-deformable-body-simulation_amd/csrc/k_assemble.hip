@@ -181,8 +181,9 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
                                                        const int* __restrict__ gn, int L,
                                                        const int* __restrict__ dOff, const int* __restrict__ aOff,
                                                        EntryKey* __restrict__ dKeys, int* __restrict__ dIds,
-                                                       float* __restrict__ dVal, unsigned* __restrict__ aKeys,
-                                                       int* __restrict__ aIds, float* __restrict__ aVal, bool skip0) {
+                                                       float* __restrict__ dVal, int* __restrict__ dEnt,
+                                                       unsigned* __restrict__ aKeys, int* __restrict__ aIds,
+                                                       float* __restrict__ aVal, bool skip0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const DevStencil s = st[i];
@@ -207,6 +208,8 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
                 dKeys[d + 1] = (EntryKey)((ot << 5) | (my & 31u));
                 dIds[d] = d;
                 dIds[d + 1] = d + 1;
+                dEnt[d] = (int)(((my & 31u) << 5) | (ot & 31u));  // FineAsm::cent (level-0 records)
+                dEnt[d + 1] = (int)(((ot & 31u) << 5) | (my & 31u));
                 for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
                 d += 2;
             }
@@ -231,8 +234,10 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
 
 // Level-0 records alone (run_level0_early): per stencil the block-entry
 // records of its same-bank pairs (level 0 of k_contact_write's loop: same
-// order, same values) at dOff[i], and its w^2 additional records at the fixed
-// slots kA0 i + it (slots past s.n keep the sentinel key).  No level ids are
+// order, same values) at dOff[i] -- keyed by their level-0 block, with the
+// entry inside the block in dEnt (the fused kernel adds a block's records in
+// order, FineAsm) -- and its w^2 additional records at the fixed slots
+// kA0 i + it (slots past s.n keep the sentinel key).  No level ids are
 // needed: a pair is a level-0 entry iff both vertices share a level-0 bank.
 constexpr int kA0 = 5;  // most vertices per stencil (EF)
 __global__ __launch_bounds__(256) void k_contact0_count(const DevStencil* __restrict__ st, int n, int* __restrict__ dCnt) {
@@ -252,8 +257,8 @@ __global__ __launch_bounds__(256) void k_contact0_count(const DevStencil* __rest
 __global__ __launch_bounds__(256) void k_contact0_write(const DevStencil* __restrict__ st, int n,
                                                         const int* __restrict__ dOff, EntryKey* __restrict__ dKeys,
                                                         int* __restrict__ dIds, float* __restrict__ dVal,
-                                                        unsigned* __restrict__ aKeys, int* __restrict__ aIds,
-                                                        float* __restrict__ aVal) {
+                                                        int* __restrict__ dEnt, unsigned* __restrict__ aKeys,
+                                                        int* __restrict__ aIds, float* __restrict__ aVal) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const DevStencil s = st[i];
@@ -272,8 +277,9 @@ __global__ __launch_bounds__(256) void k_contact0_write(const DevStencil* __rest
             if ((my >> 5) != (ot >> 5)) continue;
             float t[9];
             contact_pair(hm, s.w[x], s.w[y], t);
-            dKeys[d] = (EntryKey)((my << 5) | (ot & 31u));
-            dKeys[d + 1] = (EntryKey)((ot << 5) | (my & 31u));
+            dKeys[d] = dKeys[d + 1] = (EntryKey)(my >> 5);  // the level-0 block
+            dEnt[d] = (int)(((my & 31u) << 5) | (ot & 31u));
+            dEnt[d + 1] = (int)(((ot & 31u) << 5) | (my & 31u));
             dIds[d] = d;
             dIds[d + 1] = d + 1;
             for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
@@ -295,6 +301,17 @@ __global__ __launch_bounds__(256) void k_contact_fine_bounds(int nD, int B, int 
     };
     const int b = blockOf(j), prev = j == 0 ? -1 : blockOf(j - 1);
     for (int k = prev + 1; k <= b; ++k) fineOff[k] = j;  // blocks (prev, b] start here
+}
+
+// The same from keys that are level-0 block ids (run_level0_early; the
+// sentinel, all ones, and any key >= nFineBlk count as past the last block).
+__global__ __launch_bounds__(256) void k_block_bounds(int n, int nFineBlk, const EntryKey* __restrict__ keys,
+                                                      int* __restrict__ off) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > n) return;
+    auto blockOf = [&](int q) { return q >= n || keys[q] >= (EntryKey)nFineBlk ? nFineBlk : (int)keys[q]; };
+    const int b = blockOf(j), prev = j == 0 ? -1 : blockOf(j - 1);
+    for (int k = prev + 1; k <= b; ++k) off[k] = j;  // blocks (prev, b] start here
 }
 
 // push records of coarse node x (a run start in the sorted additional keys):
@@ -660,17 +677,6 @@ struct NodeRow {  // a row-major 9-float row per node (additional)
     static constexpr bool kFromZero = false;
     __device__ bool live(unsigned) const { return true; }
     __device__ float* at(unsigned k, int) const { return base + 9 * (size_t)k; }
-};
-// a row-major 3x3 per level-0 entry run (row < begin1), folded from zero and
-// stored at the run's first sorted position (FineAsm::cval): no memset, and
-// launched over all records so the host needs no count (coarse runs skipped)
-struct RunSlot {
-    float* base;
-    unsigned begin1;
-    static constexpr int kStride = 3;
-    static constexpr bool kFromZero = true;
-    __device__ bool live(EntryKey k) const { return (k >> RecKey::kLaneBits) < begin1; }
-    __device__ float* at(EntryKey, int start) const { return base + 9 * (size_t)start; }
 };
 
 // One wave per 64 sorted positions: the lanes find the runs starting there;
@@ -1059,15 +1065,15 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     const size_t d1 = nD > 0 ? nD : 1, a1 = nA > 0 ? nA : 1;
     if ((rc = ensure(h, h->cdKeys, d1 * 4)) || (rc = ensure(h, h->cdKeysS, d1 * 4)) ||
         (rc = ensure(h, h->cdIds, d1 * 4)) || (rc = ensure(h, h->cdIdsS, d1 * 4)) ||
-        (rc = ensure(h, h->cdVal, d1 * 36)) || (rc = ensure(h, h->caKeys, a1 * 4)) ||
+        (rc = ensure(h, h->cdVal, d1 * 36)) || (rc = ensure(h, h->cdEnt, d1 * 4)) || (rc = ensure(h, h->caKeys, a1 * 4)) ||
         (rc = ensure(h, h->caKeysS, a1 * 4)) || (rc = ensure(h, h->caIds, a1 * 4)) ||
         (rc = ensure(h, h->caIdsS, a1 * 4)) || (rc = ensure(h, h->caVal, a1 * 36)) ||
         (rc = ensure(h, h->cpCnt, (a1 + 1) * 4)) || (rc = ensure(h, h->cpOff, (a1 + 1) * 4)))
         return rc;
     k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdOff), P<int>(h->caOff),
                                                  P<EntryKey>(h->cdKeys), P<int>(h->cdIds),
-                                                 P<float>(h->cdVal), P<unsigned>(h->caKeys), P<int>(h->caIds),
-                                                 P<float>(h->caVal), skip0);
+                                                 P<float>(h->cdVal), P<int>(h->cdEnt), P<unsigned>(h->caKeys),
+                                                 P<int>(h->caIds), P<float>(h->caVal), skip0);
     if ((rc = sort_pairs(h, P<EntryKey>(h->cdKeys), P<EntryKey>(h->cdKeysS), P<int>(h->cdIds),
                          P<int>(h->cdIdsS), nD, B + RecKey::kLaneBits, s, "contact entry sort")) ||
         (rc = sort_pairs(h, P<unsigned>(h->caKeys), P<unsigned>(h->caKeysS), P<int>(h->caIds), P<int>(h->caIdsS), nA,
@@ -1087,16 +1093,12 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
                       RecKey::kLaneBits};
     if (h->factorVariant >= 4 && !skip0) {
         if (nD > 0) {
-            // each level-0 entry's contact run folded from zero once (the fused
-            // kernel adds it to its zero entry)
-            if ((rc = ensure(h, h->cFineVal, (size_t)nD * 36))) return rc;
-            k_fold_runs<RunSlot, true, EntryKey><<<cdiv(nD, 64), 64, 0, s>>>(
-                nD, ~0u, P<EntryKey>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal),
-                RunSlot{P<float>(h->cFineVal), (unsigned)begin1});
-            fa.ckeys = P<EntryKey>(h->cdKeysS);
-            fa.cval = P<float>(h->cFineVal);
+            // the level-0 records lead the entry-sorted array (rows < begin1),
+            // each entry's in stencil order: the fused kernel adds them per block
             fa.coff = P<int>(h->cFineOff);
-            fa.B = RecKey::kLaneBits;
+            fa.cids = P<int>(h->cdIdsS);
+            fa.cent = P<int>(h->cdEnt);
+            fa.cvals = P<float>(h->cdVal);
         }
         // the level-0 blocks need nothing below (pushes and coarse entries):
         // they start now, before the push count's host round trip
@@ -1182,17 +1184,19 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
         (rc = hip_check(h, hipMemsetAsync(h->add0.p, 0, (size_t)nv32 * 36, ps), "memset add0")))
         return rc;
     FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges,
-               P<float>(h->add0), nullptr, nullptr, nullptr, 0, nullptr};
+               P<float>(h->add0), nullptr, nullptr, nullptr, nullptr, nullptr};
     if (n > 0) {
-        const size_t ubD = (size_t)n * kA0 * (kA0 - 1), ubA = (size_t)n * kA0;  // 2 C(5, 2) entries, 5 rows per stencil
+        // record bounds: 2 C(5, 2) = 20 block entries per EF stencil, 2 C(4, 2) = 12 per EE / VF
+        // stencil (the sort runs over all of them); kA0 rows per stencil
+        const size_t ubD = (size_t)h->nStencilEF * 20 + (size_t)(n - h->nStencilEF) * 12, ubA = (size_t)n * kA0;
         if (ubD > 0x7fffffff) return fail(h, MAS_ERR_ARG, "too many contact stencils");
         if ((rc = ensure(h, h->c0Cnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->c0Off, (size_t)(n + 1) * 4)) ||
             (rc = ensure(h, h->c0Keys, ubD * 4)) || (rc = ensure(h, h->c0KeysS, ubD * 4)) ||
             (rc = ensure(h, h->c0Ids, ubD * 4)) || (rc = ensure(h, h->c0IdsS, ubD * 4)) ||
-            (rc = ensure(h, h->c0Val, ubD * 36)) || (rc = ensure(h, h->a0Keys, ubA * 4)) ||
-            (rc = ensure(h, h->a0KeysS, ubA * 4)) || (rc = ensure(h, h->a0Ids, ubA * 4)) ||
-            (rc = ensure(h, h->a0IdsS, ubA * 4)) || (rc = ensure(h, h->a0Val, ubA * 36)) ||
-            (rc = ensure(h, h->cFineVal, ubD * 36)) || (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4)))
+            (rc = ensure(h, h->c0Val, ubD * 36)) || (rc = ensure(h, h->c0Ent, ubD * 4)) ||
+            (rc = ensure(h, h->a0Keys, ubA * 4)) || (rc = ensure(h, h->a0KeysS, ubA * 4)) ||
+            (rc = ensure(h, h->a0Ids, ubA * 4)) || (rc = ensure(h, h->a0IdsS, ubA * 4)) ||
+            (rc = ensure(h, h->a0Val, ubA * 36)) || (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4)))
             return rc;
         // sentinel keys past the records; their ids index record 0 (never
         // folded: a sentinel is dead, but no index is left undefined)
@@ -1207,30 +1211,28 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
         if ((rc = rs_exclusive_scan(h, P<int>(h->c0Cnt), P<int>(h->c0Off), n + 1, ps, "level-0 contact scan", true)))
             return rc;
         k_contact0_write<<<cdiv(n, 256), 256, 0, ps>>>(st, n, P<int>(h->c0Off), P<EntryKey>(h->c0Keys),
-                                                       P<int>(h->c0Ids), P<float>(h->c0Val), P<unsigned>(h->a0Keys),
-                                                       P<int>(h->a0Ids), P<float>(h->a0Val));
-        // one bit above the largest real key: the sentinel (all ones) sorts
-        // after every real key instead of tying with one (the row sentinels
-        // sit between real records, and a tie would split a run)
+                                                       P<int>(h->c0Ids), P<float>(h->c0Val), P<int>(h->c0Ent),
+                                                       P<unsigned>(h->a0Keys), P<int>(h->a0Ids), P<float>(h->a0Val));
+        // block-entry records by level-0 block (stable: stencil order inside a
+        // block, so inside every entry), one bit above the largest block id
+        // so the sentinel (all ones) sorts last instead of tying with one;
+        // additional rows by vertex, the same way
+        const int bb = bit_width((unsigned)h->nFineBlk);
         const int vb = std::max(1, bit_width((unsigned)(nv32 - 1))) + 1;
         if ((rc = rs_sort_pairs(h, P<EntryKey>(h->c0Keys), P<EntryKey>(h->c0KeysS), P<int>(h->c0Ids),
-                                P<int>(h->c0IdsS), (int)ubD, vb + RecKey::kLaneBits, ps, "level-0 contact entry sort",
-                                true)) ||
+                                P<int>(h->c0IdsS), (int)ubD, bb, ps, "level-0 contact record sort", true)) ||
             (rc = rs_sort_pairs(h, P<unsigned>(h->a0Keys), P<unsigned>(h->a0KeysS), P<int>(h->a0Ids),
                                 P<int>(h->a0IdsS), (int)ubA, vb, ps, "level-0 contact row sort", true)))
             return rc;
-        k_contact_fine_bounds<<<cdiv(ubD + 1, 256), 256, 0, ps>>>((int)ubD, RecKey::kLaneBits, nv32, h->nFineBlk,
-                                                                 P<EntryKey>(h->c0KeysS), P<int>(h->cFineOff));
+        k_block_bounds<<<cdiv(ubD + 1, 256), 256, 0, ps>>>((int)ubD, h->nFineBlk, P<EntryKey>(h->c0KeysS),
+                                                          P<int>(h->cFineOff));
         k_fold_runs<NodeRow, true, unsigned><<<cdiv(ubA, 64), 64, 0, ps>>>(
             (int)ubA, 0xffffffffu, P<unsigned>(h->a0KeysS), P<int>(h->a0IdsS), P<float>(h->a0Val),
             NodeRow{P<float>(h->add0)});
-        k_fold_runs<RunSlot, true, EntryKey><<<cdiv(ubD, 64), 64, 0, ps>>>(
-            (int)ubD, ~0u, P<EntryKey>(h->c0KeysS), P<int>(h->c0IdsS), P<float>(h->c0Val),
-            RunSlot{P<float>(h->cFineVal), (unsigned)nv32});
-        fa.ckeys = P<EntryKey>(h->c0KeysS);
-        fa.cval = P<float>(h->cFineVal);
         fa.coff = P<int>(h->cFineOff);
-        fa.B = RecKey::kLaneBits;
+        fa.cids = P<int>(h->c0IdsS);
+        fa.cent = P<int>(h->c0Ent);
+        fa.cvals = P<float>(h->c0Val);
     }
     // earlyOd (A/B, env MAS_EARLY_OD): od and the record counts need only
     // level-0 data too and can run here, ahead of the fused kernel, instead of
@@ -1312,7 +1314,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     FineContacts fc{};
     // level-0 additional rows: add0 when run_level0_early built them
     FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges,
-               h->earlyFused ? P<float>(h->add0) : add, nullptr, nullptr, nullptr, 0,
+               h->earlyFused ? P<float>(h->add0) : add, nullptr, nullptr, nullptr, nullptr,
                h->cfg.keep_blocks ? dense : nullptr};
     bool forked = false;
     if (h->nStencil && (rc = run_contacts(h, s, fc, fa, forked))) return rc;

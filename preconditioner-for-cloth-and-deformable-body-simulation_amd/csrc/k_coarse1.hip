@@ -105,6 +105,7 @@ struct Coarse1Args {
     const int* done;      // PCG: exit at once when set
     int pollLimit;        // polls before a wait gives up (kPollLimit; < 0: give up at once, a test knob)
     int* timeouts;        // waits that gave up: this apply's z is incomplete (mas_stats.wait_timeouts)
+    const int2* members;  // grouped level 3: per coarse node (child bank, child mask); null: the reference's fold
 };
 
 union C1Shared {
@@ -159,7 +160,8 @@ __device__ __forceinline__ void bank_wave(const Coarse1Args& a, int B, C1Shared&
             }
         }
     }
-    if (a.L >= 4 && own && info.z >= 0) st_tag(a.tR1 + info.z, ax, ay, az, a.epoch);  // the level-3 fold's input
+    if (a.L >= 4 && !a.members && own && info.z >= 0)  // the reference-order level-3 fold's input
+        st_tag(a.tR1 + info.z, ax, ay, az, a.epoch);
     if (lane < 32) sh.bank.red[j] = make_float4(ax, ay, az, 0.f);
     __builtin_amdgcn_wave_barrier();
     // R2 of the level-2 nodes whose children are this bank's components (their lowest lane)
@@ -263,6 +265,40 @@ __device__ __forceinline__ void fold_wave(const Coarse1Args& a, int T, C1Shared&
     C1_STAMP(0, T, 3);
 }
 
+// grouped level 3 (mas_config.reference_restriction = 0): node T's R3 is its
+// children's R2 -- the lanes of one component of one level-2 bank -- folded
+// in lane (= level-2 id) order from +0, as k_solve123g; lane j polls child
+// j's tagged R2 until every child's has this apply's tag
+__device__ __forceinline__ void fold_wave_grouped(const Coarse1Args& a, int T) {
+    const int lane = threadIdx.x & 63, j = lane & 31;
+    const int2 mb = a.members[a.lv3Begin + T - a.begin1];  // (level-2 bank, children)
+    const bool child = lane < 32 && (((unsigned)mb.y >> j) & 1u);
+    unsigned long long v[3] = {0ull, 0ull, 0ull};
+    bool ok = !child;
+    for (int d = 0; d < a.pollDelay; ++d) __builtin_amdgcn_s_sleep(64);
+    for (int polls = 0; polls <= a.pollLimit; ++polls) {
+        if (!ok) {
+            ld_tag(a.tR2 + mb.x * 32 + j, v);
+            ok = tag_ok(v, a.epoch);
+        }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (!__all(ok) && lane == 0) atomicAdd(a.timeouts, 1);  // R3 from stale R2: counted
+    const float x = child ? tag_val(v[0]) : 0.f, y = child ? tag_val(v[1]) : 0.f, z = child ? tag_val(v[2]) : 0.f;
+    float ax = 0.f, ay = 0.f, az = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        ax = __fadd_rn(ax, __shfl(x, k));
+        ay = __fadd_rn(ay, __shfl(y, k));
+        az = __fadd_rn(az, __shfl(z, k));
+    }
+    if (lane == 0) {
+        st_tag(a.tR3 + T, ax, ay, az, a.epoch);
+        a.rc[a.lv3Begin + T - a.begin1] = make_float4(ax, ay, az, 0.f);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // level-2 / level-3 block: poll its 32 R, then Z = Inv R
 // ---------------------------------------------------------------------------
@@ -302,7 +338,7 @@ __global__ __launch_bounds__(64) void k_coarse1(Coarse1Args a) {
     int w = blockIdx.x;  // workgroup-uniform roles
     if (w < a.nb1) return bank_wave(a, w, sh);
     w -= a.nb1;
-    if (w < a.n3) return fold_wave(a, w, sh);
+    if (w < a.n3) return a.members ? fold_wave_grouped(a, w) : fold_wave(a, w, sh);
     w -= a.n3;
     if (w < a.nb2) return solve_wave(a, a.lv2Begin / 32 + w, a.lv2Begin, a.n2, a.tR2, w);
     w -= a.nb2;
@@ -378,6 +414,7 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.pollDelay = h->c1PollDelay;
     a.done = h->applyDone;
     a.pollLimit = h->c1PollLimit;
+    a.members = h->groupedR3 && deep ? P<int2>(h->members) : nullptr;
     a.timeouts = P<int>(h->devStatus) + 2;
     h->c1Launched = true;
     k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3, 64, 0, s>>>(a);

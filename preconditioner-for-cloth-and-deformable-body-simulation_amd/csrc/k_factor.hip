@@ -472,23 +472,36 @@ __device__ __forceinline__ void build_slab(const FineAsm& a, int blk, float* S, 
     float4* S4 = reinterpret_cast<float4*>(S);
     for (int q = lane; q < 48 * 96 / 4; q += 64) S4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
-    if (a.ckeys) {  // contact entries of rows in this slab: distinct keys -> distinct entries
-        const int j1 = a.coff[blk + 1];
-        const unsigned colMask = (1u << a.B) - 1;
-        for (int j = a.coff[blk] + lane; j < j1; j += 64) {
-            const unsigned key = a.ckeys[j];
-            const bool start = j == 0 || a.ckeys[j - 1] != key;
-            const int nl = (int)((key >> a.B) & 31) - 16 * H, col = (int)(key & colMask) & 31;
-            if (start && nl >= 0 && nl < 16) {
-                const float* src = a.cval + 9 * (size_t)j;
-                float* e = S + (3 * nl) * 96 + 3 * col;
+    if (a.coff) {
+        // the block's contact records, 16 at a time staged past the slab in
+        // M's LDS (entry code + 9 values each); lane q < 9 adds component q
+        // (column-major: row q % 3, column q / 3) of every record in order, so
+        // each entry gets its records in stencil order, added to the zero
+        // entry before the CSR terms (.cpp:88-97)
+        float* stg = S + 48 * 96;
+        const int q = lane < 9 ? lane : 0, qr = q % 3, qc = q / 3;
+        const int j0 = a.coff[blk], j1 = a.coff[blk + 1];
+        for (int jb = j0; jb < j1; jb += 16) {
+            const int cnt = min(16, j1 - jb);
+            if (lane < cnt) {
+                const int id = a.cids[jb + lane];
+                stg[10 * lane] = __int_as_float(a.cent[id]);
+                const float* src = a.cvals + 9 * (size_t)id;
 #pragma unroll
-                for (int r = 0; r < 3; ++r)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], src[3 * r + c]);
+                for (int e = 0; e < 9; ++e) stg[10 * lane + 1 + e] = src[e];
             }
+            __syncthreads();
+            if (lane < 9)
+                for (int k = 0; k < cnt; ++k) {
+                    const int ent = __float_as_int(stg[10 * k]);
+                    const int nl = (ent >> 5) - 16 * H, col = ent & 31;
+                    if (nl >= 0 && nl < 16) {
+                        float* p = S + (3 * nl + qr) * 96 + 3 * col + qc;
+                        *p = __fadd_rn(*p, stg[10 * k + 1 + q]);
+                    }
+                }
+            __syncthreads();
         }
-        __syncthreads();
     }
     // CSR terms: lane = (node n = lane % 16, slot group g = lane / 16), ELL slot
     // k = k0 + g + 4 p; a pass loads 4 slots per lane, then adds them in slot order
@@ -573,7 +586,7 @@ template <bool MFMA>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_fused(
     FineAsm a, float* __restrict__ inv, const uint4* __restrict__ tileSlot, const uint4* __restrict__ valuSlot,
     int blk0, int* __restrict__ status) {
-    static_assert(48 * 96 <= kPackedM, "a slab fits in M's LDS");
+    static_assert(48 * 96 + 16 * 10 <= kPackedM, "a slab and 16 staged contact records fit in M's LDS");
     __shared__ __attribute__((aligned(16))) float M[kPackedM];
     __shared__ __attribute__((aligned(16))) float piv[96];
     __shared__ float dinv[96];

@@ -302,13 +302,27 @@ __global__ __launch_bounds__(256) void k_hier_check(const DevStencil* __restrict
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const DevStencil s = st[i];
+    // every vertex's node at every level first (independent loads), so the
+    // walk below waits for one round trip instead of one per level
+    // (static indices throughout: the arrays stay in registers)
+    unsigned node[5][kMaxLevels];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        node[k][0] = (unsigned)s.idx[k];
+#pragma unroll
+        for (int l = 1; l < kMaxLevels; ++l)
+            node[k][l] = k < s.n && l < a.L ? (unsigned)a.cst[(size_t)(l - 1) * a.nV + s.idx[k]] : 0u;
+    }
     int dirty = a.L;
-    for (int x = 0; x < s.nFirst; ++x)
-        for (int y = s.nFirst; y < s.n; ++y) {
-            const int vx = s.idx[x], vy = s.idx[y];
-            for (int l = 0; l < a.L && l < dirty; ++l) {
-                const unsigned my = l ? (unsigned)a.cst[(size_t)(l - 1) * a.nV + vx] : (unsigned)vx;
-                const unsigned ot = l ? (unsigned)a.cst[(size_t)(l - 1) * a.nV + vy] : (unsigned)vy;
+#pragma unroll
+    for (int x = 0; x < 5; ++x)
+#pragma unroll
+        for (int y = 1; y < 5; ++y) {
+            if (!(y > x && x < s.nFirst && y >= s.nFirst && y < s.n)) continue;
+#pragma unroll
+            for (int l = 0; l < kMaxLevels; ++l) {
+                if (l >= a.L || l >= dirty) break;
+                const unsigned my = node[x][l], ot = node[y][l];
                 if (my == ot) break;             // one node from here up
                 if ((my >> 5) != (ot >> 5)) continue;  // not connected at this level
                 const unsigned m = l ? a.coarseMask[a.maskBase[l] + my] : a.fine[my];
@@ -365,7 +379,7 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
     if (efNum < 0 || eeNum < 0 || vfNum < 0) return fail(h, MAS_ERR_HIP, "reading contact counts");
     long long total = efNum + eeNum + vfNum;
     const long long maxStencil = (long long)h->nV * 32;  // .cpp:187-188
-    h->nStencil = 0;
+    h->nStencil = h->nStencilEF = 0;
     if (total <= 0) return MAS_OK;
     if ((efNum && !ef) || (eeNum && !ee) || (vfNum && !vf)) return fail(h, MAS_ERR_ARG, "contact records missing");
     if ((efNum || eeNum) && !h->edges.p) return fail(h, MAS_ERR_ARG, "EF/EE contacts need m_edges");
@@ -405,6 +419,7 @@ int build_stencils(mas_context* h, const void* ef, const void* ee, const void* v
                                                  P<int>(h->stencilSlots), P<int4>(h->edges), P<int4>(h->faces),
                                                  P<int>(h->o2s), h->cfg.fix_vf_bary, P<DevStencil>(h->stencils));
     h->nStencil = valid;
+    h->nStencilEF = (int)std::min<long long>(valid, efNum);  // the EF stencils come first (5 vertices each)
     return hip_check(h, hipGetLastError(), "stencil kernels");
 }
 

@@ -211,6 +211,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
 
 int mas_destroy(mas_handle h) {
     if (!h) return MAS_ERR_ARG;
+    h->prepWorker.reset();  // idle between Prepares: joined before anything it used goes
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     // drain every stream this handle enqueued on -- including an allgather of

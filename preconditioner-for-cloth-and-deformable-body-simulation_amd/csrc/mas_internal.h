@@ -15,10 +15,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdint>
 #include <functional>
 #include <initializer_list>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mas_capi.h"
@@ -56,8 +60,8 @@ struct DeepArgs {
 // Level-0 assembly inputs of the fused assemble + factor kernel (k_factor.hip)
 // and the od kernel (k_assemble.hip): the CSR Hessian in the sorted vertex
 // order's ELL neighbour table, the contact rows (`additional`), and the
-// block-entry contact sums of the level-0 blocks, one prefolded 3x3 per
-// distinct entry key at the position its run starts in the sorted records.
+// level-0 blocks' contact block-entry records, grouped by block with every
+// entry's records in stencil order (a stable sort by block, or by entry).
 struct FineAsm {
     int nV, maxNbr;
     const int* s2o;
@@ -67,10 +71,10 @@ struct FineAsm {
     const float* off9;
     const int* ranges;
     const float* additional;
-    const unsigned* ckeys;            // sorted block-entry keys row * 32 + (col & 31) (null: no contacts)
-    const float* cval;                // row-major 3x3 per run start
-    const int* coff;                  // per level-0 block: first record (nFineBlk + 1)
-    int B;
+    const int* coff;                  // per level-0 block: its records [coff[b], coff[b + 1]) (null: no contacts)
+    const int* cids;                  // sorted position -> record id
+    const int* cent;                  // per record id: (row & 31) * 32 + (col & 31) inside its block
+    const float* cvals;               // per record id: the 3x3, column-major
     float* keep;                      // dense base: also store the assembled blocks (null: not kept)
 };
 
@@ -94,6 +98,61 @@ struct ScopedEvents {
     ScopedEvents(const ScopedEvents&) = delete;
     ScopedEvents& operator=(const ScopedEvents&) = delete;
     bool ok() const { return e[0] && e[1]; }
+};
+
+// A host thread kept for the handle's lifetime that queues Prepare's early
+// level-0 path on prepStream while the caller's thread queues the rest
+// (prepare.hip).  Creating a thread per Prepare cost ~100 us before its first
+// launch (thread start + HIP's per-thread state).  HIP's current device is
+// per host thread: every job runs after hipSetDevice(device).
+class PrepWorker {
+  public:
+    explicit PrepWorker(int device) : device_(device), t_([this] { loop(); }) {}
+    ~PrepWorker() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        t_.join();
+    }
+    PrepWorker(const PrepWorker&) = delete;
+    PrepWorker& operator=(const PrepWorker&) = delete;
+    // job(devOk): devOk = hipSetDevice succeeded on the worker
+    void post(std::function<void(bool)> job) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = std::move(job);
+            busy_ = true;
+        }
+        cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [this] { return !busy_; });
+    }
+
+  private:
+    void loop() {
+        std::unique_lock<std::mutex> g(m_);
+        for (;;) {
+            cv_.wait(g, [this] { return stop_ || (busy_ && job_); });
+            if (stop_) return;
+            std::function<void(bool)> job = std::move(job_);
+            job_ = nullptr;
+            g.unlock();
+            job(hipSetDevice(device_) == hipSuccess);
+            g.lock();
+            busy_ = false;
+            cv_.notify_all();
+        }
+    }
+    int device_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::function<void(bool)> job_;
+    bool busy_ = false, stop_ = false;
+    std::thread t_;  // last: starts after the members above exist
 };
 
 }  // namespace mas
@@ -121,7 +180,7 @@ struct mas_context {
     // hand-offs (k_coarse1.hip, L >= 3); 2 = two launches, restrictions then
     // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (The
     // side-stream overlap was measured slower: DESIGN.md section 4.)
-    int coarseMode = -1;  // -1: 3 at L = 3, 2 at L >= 4 (measured)
+    int coarseMode = -1;  // -1: 3 at L = 3 and with the grouped level 3, else 2 (measured)
     // level-3 residual (mas_config.reference_restriction, env MAS_REF_RESTRICT):
     // true = the sum of its children's R2 (default), false = the reference's
     // fold of every R1 in level-1 id order (deep_fold.h)
@@ -137,6 +196,7 @@ struct mas_context {
     // 0 = default-policy loads (A/B)
     int fineVariant = 1;
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
+    int nStencilEF = 0;  // of nStencil, the EF stencils (at most 5 vertices; EE / VF have 4)
     int nBlkPrev = 0;  // nBlk of the previous Prepare, read by the early path's thread (run_levels may change nBlk meanwhile)
     // sharded Prepare (mas_set_prepare_shard): the next Prepare assembles and
     // factors only the level-0 blocks of Morton shard prepRank / prepWorld;
@@ -158,7 +218,6 @@ struct mas_context {
     // variant); denseBase = the address block 0 would have (dense_base()).
     mas::Buffer dense, inv, slotTable, tileSlot, valuSlot;
     bool denseFine = false;  // the last Prepare stored the level-0 blocks
-    mas::Buffer cFineVal;    // prefolded level-0 contact entries (FineAsm::cval)
     hipStream_t prepStream = nullptr;  // fused level-0 assemble + factor, beside the coarse assembly
     hipEvent_t evPrepFork = nullptr, evPrepJoin = nullptr;
     hipEvent_t evFine[2] = {nullptr, nullptr};  // timing of the fused level-0 kernel (prepare_fine_ms)
@@ -167,9 +226,13 @@ struct mas_context {
     // the stencils and the fused kernel starts there, beside the level build;
     // add0 = level-0 additional rows, evAdd0 = they are ready (k_od waits)
     bool earlyFused = false;
-    int prepCuReserve = 64;  // CUs the fused kernel's queue leaves to the caller's stream (env MAS_PREP_CU_RESERVE)
+    // CUs the fused kernel's queue leaves to the caller's stream (env
+    // MAS_PREP_CU_RESERVE): 32 since the level maps are reused (1M + contacts,
+    // one box: 0 / 16 / 32 / 48 / 64 -> 3.06 / 3.21 / 2.69 / 2.88 / 2.90 ms)
+    int prepCuReserve = 32;
     int fusedAfterLevels = 0;  // A/B (env MAS_FUSED_AFTER_LEVELS): the early fused kernel waits for the level build
     int earlyThread = 1;       // the early path queued from a second host thread (env MAS_EARLY_THREAD)
+    std::unique_ptr<mas::PrepWorker> prepWorker;  // that thread (created by the first Prepare that needs it)
     int earlyOd = 0;           // A/B (env MAS_EARLY_OD): k_od in the early path
     bool odDone = false;       // this Prepare's od / record counts are queued already
     mas::FineAsm earlyFa{};    // its inputs, kept for launch_level0_fused
@@ -178,7 +241,8 @@ struct mas_context {
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, tab, termCnt;
     // contact records (k_assemble.hip): block entries (d*), additional rows (a*), pushes (p*)
-    mas::Buffer cdCnt, cdOff, cdKeys, cdKeysS, cdIds, cdIdsS, cdVal, cFineOff;
+    mas::Buffer cdCnt, cdOff, cdKeys, cdKeysS, cdIds, cdIdsS, cdVal, cdEnt, cFineOff;
+    mas::Buffer c0Ent;  // entry code per level-0 contact record (FineAsm::cent)
     mas::Buffer caCnt, caOff, caKeys, caKeysS, caIds, caIdsS, caVal;
     mas::Buffer cpCnt, cpOff, cpKeys, cpKeysS, cpIds, cpIdsS;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, shardPos1, l1src;
@@ -280,7 +344,7 @@ struct mas_context {
                               &cst, &goingNext, &vmap, &coarseTables, &dense, &inv, &slotTable, &tileSlot, &valuSlot, &additional, &od,
                               &recCnt, &recOff, &rec, &recKeys, &recKeysSorted, &recIds, &recIdsSorted, &vkeys,
                               &tab, &termCnt,
-                              &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cFineVal, &caCnt, &caOff,
+                              &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cdEnt, &c0Ent, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
                               &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart, &rsKeysP, &rsValsP, &rsHistP, &rsPartP, &add0, &c0Cnt, &c0Off, &c0Keys, &c0KeysS, &c0Ids, &c0IdsS,

@@ -1,7 +1,5 @@
 // prepare.hip -- PreparePreconditioner orchestration (.cpp:67-98):
 // stencils -> aggregation levels -> block assembly -> batched factor -> apply tables.
-#include <thread>
-
 #include "mas_internal.h"
 
 namespace mas {
@@ -40,14 +38,15 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     if (early && h->earlyThread) {
         // a second host thread queues prepStream's work while this one queues
         // the level build: each stream is fed from the start (one thread
-        // queueing both left the early path behind the level kernels).  HIP's
-        // current device is per host thread: the new thread selects the
-        // handle's first (ensure() allocates on the current device).  Its
-        // error message is stored by this thread after the join.
+        // queueing both left the early path behind the level kernels): the
+        // handle's PrepWorker, which selects the handle's device first
+        // (ensure() allocates on the current device).  Its error message is
+        // stored by this thread after the wait.
         int earlyRc = MAS_OK;
         std::string earlyErr;
-        std::thread t([&]() {
-            if (hipSetDevice(h->device) != hipSuccess) {
+        if (!h->prepWorker) h->prepWorker = std::make_unique<PrepWorker>(h->device);
+        h->prepWorker->post([&](bool devOk) {
+            if (!devOk) {
                 earlyRc = MAS_ERR_HIP;
                 earlyErr = "early Prepare thread: hipSetDevice failed";
                 return;
@@ -56,7 +55,7 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
             earlyRc = run_level0_early(h, d_diag9, d_off9, d_ranges, s);
         });
         rc = run_levels(h, s, d_ranges);
-        t.join();
+        h->prepWorker->wait();
         if (rc) return rc;
         if (earlyRc) return fail(h, earlyRc, earlyErr);
     } else if ((rc = run_levels(h, s, d_ranges, [&]() {
