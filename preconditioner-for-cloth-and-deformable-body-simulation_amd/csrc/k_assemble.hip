@@ -148,11 +148,40 @@ __global__ __launch_bounds__(64) void k_contact_terms(const float* __restrict__ 
         }
 }
 
+// A stencil's vertices at every level, from the per-vertex ancestor table
+// (coarseTables: the level-1..4 ancestors, AggregationKernel .cpp:1119-1147):
+// five independent 16-byte loads instead of the dependent goingNext walk of
+// each pair (AdditionalSchwarzHessian2's while loop, .cpp:1171-1176).
+// nd[k][l] = vertex k's node at level l (l <= min(L - 1, 4)).
+__device__ __forceinline__ void stencil_nodes(const DevStencil& s, const int4* __restrict__ anc, unsigned (&nd)[5][5]) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int4 a = k < s.n ? anc[s.idx[k]] : make_int4(0, 0, 0, 0);
+        nd[k][0] = (unsigned)s.idx[k];
+        nd[k][1] = (unsigned)a.x;
+        nd[k][2] = (unsigned)a.y;
+        nd[k][3] = (unsigned)a.z;
+        nd[k][4] = (unsigned)a.w;
+    }
+}
+// the first level where vertices x and y share a bank (L: none); my / ot their nodes there
+__device__ __forceinline__ int climb_nodes(const unsigned (&nd)[5][5], int x, int y, int L, unsigned& my,
+                                           unsigned& ot) {
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        if (l >= L) break;
+        my = nd[x][l];
+        ot = nd[y][l];
+        if ((my >> 5) == (ot >> 5)) return l;
+    }
+    return L;
+}
+
 // counts: dCnt[i] block-entry records, aCnt[i] additional records of stencil i
 // skip0: without the level-0 records (block entries of same-bank pairs, the
 // w^2 additional rows), which run_level0_early built already
 __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restrict__ st, int n,
-                                                       const int* __restrict__ gn, int L, int* __restrict__ dCnt,
+                                                       const int4* __restrict__ anc, int L, int* __restrict__ dCnt,
                                                        int* __restrict__ aCnt, bool skip0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
@@ -161,14 +190,19 @@ __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restr
         return;
     }
     const DevStencil s = st[i];
+    unsigned nd[5][5];
+    stencil_nodes(s, anc, nd);
     int d = 0, a = skip0 ? 0 : s.n;
-    for (int x = 0; x < s.n; ++x)
-        for (int y = x + 1; y < s.n; ++y) {
-            unsigned my = (unsigned)s.idx[x], ot = (unsigned)s.idx[y];
-            const int level = climb(gn, L, my, ot);
+#pragma unroll
+    for (int x = 0; x < 5; ++x)
+#pragma unroll
+        for (int y = 1; y < 5; ++y) {
+            if (y <= x || y >= s.n) continue;
+            unsigned my = 0, ot = 0;
+            const int level = climb_nodes(nd, x, y, L, my, ot);
             if (level >= L) continue;
             if (level > 0 || !skip0) d += 2;
-            if (level < L - 1) a += gn[my] == gn[ot] ? 1 : 2;
+            if (level < L - 1) a += nd[x][level + 1] == nd[y][level + 1] ? 1 : 2;
         }
     dCnt[i] = d;
     aCnt[i] = a;
@@ -178,15 +212,17 @@ __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restr
 // keys: block entry my * 32 + (ot & 31) (RecKey with begin1 = 0: the pair
 // shares a bank at its level), additional node id.
 __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restrict__ st, int n,
-                                                       const int* __restrict__ gn, int L,
+                                                       const int4* __restrict__ anc, int L,
                                                        const int* __restrict__ dOff, const int* __restrict__ aOff,
                                                        EntryKey* __restrict__ dKeys, int* __restrict__ dIds,
                                                        float* __restrict__ dVal, int* __restrict__ dEnt,
                                                        unsigned* __restrict__ aKeys, int* __restrict__ aIds,
-                                                       float* __restrict__ aVal, bool skip0) {
+                                                       float* __restrict__ aVal, bool skip0, unsigned kb) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const DevStencil s = st[i];
+    unsigned nd[5][5];
+    stencil_nodes(s, anc, nd);
     float hm[9];
     contact_h(s, hm);
     int d = dOff[i], a = aOff[i];
@@ -195,17 +231,21 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
         aIds[a] = a;
         contact_self(hm, s.w[it], aVal + 9 * (size_t)a);
     }
-    for (int x = 0; x < s.n; ++x)
-        for (int y = x + 1; y < s.n; ++y) {
-            unsigned my = (unsigned)s.idx[x], ot = (unsigned)s.idx[y];
-            const int level = climb(gn, L, my, ot);
+#pragma unroll
+    for (int x = 0; x < 5; ++x)
+#pragma unroll
+        for (int y = 1; y < 5; ++y) {
+            if (y <= x || y >= s.n) continue;
+            unsigned my = 0, ot = 0;
+            const int level = climb_nodes(nd, x, y, L, my, ot);
             if (level >= L) continue;
             float t[9];
             contact_pair(hm, s.w[x], s.w[y], t);
             if (level > 0 || !skip0) {
-                // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot]
-                dKeys[d] = (EntryKey)((my << 5) | (ot & 31u));
-                dKeys[d + 1] = (EntryKey)((ot << 5) | (my & 31u));
+                // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot];
+                // rows relative to kb (begin_1 when only coarse records are written)
+                dKeys[d] = (EntryKey)(((my - kb) << 5) | (ot & 31u));
+                dKeys[d + 1] = (EntryKey)(((ot - kb) << 5) | (my & 31u));
                 dIds[d] = d;
                 dIds[d + 1] = d + 1;
                 dEnt[d] = (int)(((my & 31u) << 5) | (ot & 31u));  // FineAsm::cent (level-0 records)
@@ -214,15 +254,15 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
                 d += 2;
             }
             if (level < L - 1) {
-                const unsigned pm = (unsigned)gn[my], po = (unsigned)gn[ot];
+                const unsigned pm = nd[x][level + 1], po = nd[y][level + 1];
                 if (pm == po) {
-                    aKeys[a] = pm;
+                    aKeys[a] = pm - kb;
                     aIds[a] = a;
                     for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = contact_double(t[e]);
                     ++a;
                 } else {
-                    aKeys[a] = pm;
-                    aKeys[a + 1] = po;
+                    aKeys[a] = pm - kb;
+                    aKeys[a + 1] = po - kb;
                     aIds[a] = a;
                     aIds[a + 1] = a + 1;
                     for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = aVal[9 * (size_t)(a + 1) + e] = t[e];
@@ -316,29 +356,31 @@ __global__ __launch_bounds__(256) void k_block_bounds(int n, int nFineBlk, const
 
 // push records of coarse node x (a run start in the sorted additional keys):
 // targets x, gn[x], ... below total
+// (keys relative to kb: node = key + kb; push keys written the same way)
 __global__ __launch_bounds__(256) void k_push_count(int nA, int begin1, int tc, const unsigned* __restrict__ aKeys,
-                                                    const int* __restrict__ gn, int* __restrict__ pCnt) {
+                                                    unsigned kb, const int* __restrict__ gn, int* __restrict__ pCnt) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > nA) return;
     int c = 0;
     if (j < nA) {
-        const unsigned x = aKeys[j];
-        if (x >= (unsigned)begin1 && (j == 0 || aKeys[j - 1] != x))
+        const unsigned x = aKeys[j] + kb;
+        if (x >= (unsigned)begin1 && (j == 0 || aKeys[j - 1] != aKeys[j]))
             for (int t = (int)x; t < tc; t = gn[t]) ++c;
     }
     pCnt[j] = c;
 }
 
 __global__ __launch_bounds__(256) void k_push_write(int nA, int begin1, int tc, const unsigned* __restrict__ aKeys,
-                                                    const int* __restrict__ gn, const int* __restrict__ pOff,
-                                                    unsigned* __restrict__ pKeys, int* __restrict__ pIds) {
+                                                    unsigned kb, const int* __restrict__ gn,
+                                                    const int* __restrict__ pOff, unsigned* __restrict__ pKeys,
+                                                    int* __restrict__ pIds) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nA) return;
-    const unsigned x = aKeys[j];
-    if (x < (unsigned)begin1 || (j > 0 && aKeys[j - 1] == x)) return;
+    const unsigned x = aKeys[j] + kb;
+    if (x < (unsigned)begin1 || (j > 0 && aKeys[j - 1] == aKeys[j])) return;
     int w = pOff[j];
     for (int t = (int)x; t < tc; t = gn[t], ++w) {
-        pKeys[w] = (unsigned)t;
+        pKeys[w] = (unsigned)t - kb;
         pIds[w] = (int)x;  // the pushed value: additional row x (row-major)
     }
 }
@@ -664,12 +706,13 @@ struct DenseEntry {  // block entry (row node, column node) of the dense buffer
     __device__ bool live(EntryKey) const { return true; }
     __device__ float* at(EntryKey k, int) const { return entry(dense, rk.row(k), rk.col(k)); }
 };
-struct DenseDiag {  // the diagonal entry of a node
+struct DenseDiag {  // the diagonal entry of node key + kb
     float* dense;
+    unsigned kb;
     static constexpr int kStride = 96;
     static constexpr bool kFromZero = false;
     __device__ bool live(unsigned) const { return true; }
-    __device__ float* at(unsigned k, int) const { return entry(dense, k, k); }
+    __device__ float* at(unsigned k, int) const { return entry(dense, k + kb, k + kb); }
 };
 struct NodeRow {  // a row-major 9-float row per node (additional)
     float* base;
@@ -1052,10 +1095,16 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     if (B + RecKey::kLaneBits > 32) return fail(h, MAS_ERR_ARG, "contact entry keys: more than 2^27 nodes");
     if ((rc = ensure(h, h->cdCnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->cdOff, (size_t)(n + 1) * 4)) ||
         (rc = ensure(h, h->caCnt, (size_t)(n + 1) * 4)) || (rc = ensure(h, h->caOff, (size_t)(n + 1) * 4)) ||
-        (!h->earlyFused && (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4))))  // prepStream's otherwise
+        (!h->earlyPlanned && (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4))))  // prepStream's otherwise
         return rc;
-    const bool skip0 = h->earlyFused;  // level-0 records built by run_level0_early
-    k_contact_count<<<cdiv(n + 1, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdCnt), P<int>(h->caCnt), skip0);
+    const bool skip0 = h->earlyPlanned;  // level-0 records built by run_level0_early (its worker may still be queueing)
+    // keys relative to kb: with only coarse records (skip0) every row, node and
+    // push target is >= begin_1, so the sorts need the bits of the coarse node
+    // count (16 at 1M) instead of all nodes' (21): one pass less per sort
+    const unsigned kb = skip0 ? (unsigned)begin1 : 0u;
+    const int Bk = skip0 ? std::max(1, bit_width((unsigned)std::max(tc - begin1 - 1, 0))) : B;
+    const int4* anc = P<int4>(h->coarseTables);
+    k_contact_count<<<cdiv(n + 1, 256), 256, 0, s>>>(st, n, anc, L, P<int>(h->cdCnt), P<int>(h->caCnt), skip0);
     if ((rc = exclusive_scan(h, P<int>(h->cdCnt), P<int>(h->cdOff), n + 1, s, "contact scan")) ||
         (rc = exclusive_scan(h, P<int>(h->caCnt), P<int>(h->caOff), n + 1, s, "contact scan")))
         return rc;
@@ -1070,14 +1119,14 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         (rc = ensure(h, h->caIdsS, a1 * 4)) || (rc = ensure(h, h->caVal, a1 * 36)) ||
         (rc = ensure(h, h->cpCnt, (a1 + 1) * 4)) || (rc = ensure(h, h->cpOff, (a1 + 1) * 4)))
         return rc;
-    k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, gn, L, P<int>(h->cdOff), P<int>(h->caOff),
+    k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, anc, L, P<int>(h->cdOff), P<int>(h->caOff),
                                                  P<EntryKey>(h->cdKeys), P<int>(h->cdIds),
                                                  P<float>(h->cdVal), P<int>(h->cdEnt), P<unsigned>(h->caKeys),
-                                                 P<int>(h->caIds), P<float>(h->caVal), skip0);
+                                                 P<int>(h->caIds), P<float>(h->caVal), skip0, kb);
     if ((rc = sort_pairs(h, P<EntryKey>(h->cdKeys), P<EntryKey>(h->cdKeysS), P<int>(h->cdIds),
-                         P<int>(h->cdIdsS), nD, B + RecKey::kLaneBits, s, "contact entry sort")) ||
+                         P<int>(h->cdIdsS), nD, Bk + RecKey::kLaneBits, s, "contact entry sort")) ||
         (rc = sort_pairs(h, P<unsigned>(h->caKeys), P<unsigned>(h->caKeysS), P<int>(h->caIds), P<int>(h->caIdsS), nA,
-                         B, s, "contact row sort")))
+                         Bk, s, "contact row sort")))
         return rc;
     float* dense = dense_base(h);
     // fine entries: k_level0_block; coarse entries: folded onto the zeroed coarse blocks
@@ -1088,7 +1137,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     if (nA > 0)
         k_fold_runs<NodeRow, true, unsigned><<<cdiv(nA, 64), 64, 0, s>>>(
             nA, 0xffffffffu, P<unsigned>(h->caKeysS), P<int>(h->caIdsS), P<float>(h->caVal),
-            NodeRow{P<float>(h->additional)});
+            NodeRow{P<float>(h->additional) + 9 * (size_t)kb});
     fc = FineContacts{P<EntryKey>(h->cdKeysS), P<int>(h->cdIdsS), P<float>(h->cdVal), P<int>(h->cFineOff),
                       RecKey::kLaneBits};
     if (h->factorVariant >= 4 && !skip0) {
@@ -1105,7 +1154,8 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         if ((rc = fork_fused(h, fa, s))) return rc;
         forked = true;
     }
-    k_push_count<<<cdiv(nA + 1, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), gn, P<int>(h->cpCnt));
+    k_push_count<<<cdiv(nA + 1, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), kb, gn,
+                                                   P<int>(h->cpCnt));
     if ((rc = exclusive_scan(h, P<int>(h->cpCnt), P<int>(h->cpOff), nA + 1, s, "push scan"))) return rc;
     int pf[2] = {0, 0};  // push count, first coarse block-entry record (0: no level-0 records here)
     if (skip0) {
@@ -1114,7 +1164,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         return rc;
     }
     const int nP = pf[0], fineEnd = pf[1];
-    const RecKey rk{0, B};
+    const RecKey rk{(int)kb, Bk};
     if (nD > fineEnd)
         k_fold_runs<DenseEntry, true, EntryKey><<<cdiv(nD - fineEnd, 64), 64, 0, s>>>(
             nD - fineEnd, ~0u, P<EntryKey>(h->cdKeysS) + fineEnd, P<int>(h->cdIdsS) + fineEnd,
@@ -1123,14 +1173,15 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
         if ((rc = ensure(h, h->cpKeys, (size_t)nP * 4)) || (rc = ensure(h, h->cpKeysS, (size_t)nP * 4)) ||
             (rc = ensure(h, h->cpIds, (size_t)nP * 4)) || (rc = ensure(h, h->cpIdsS, (size_t)nP * 4)))
             return rc;
-        k_push_write<<<cdiv(nA, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), gn, P<int>(h->cpOff),
-                                                   P<unsigned>(h->cpKeys), P<int>(h->cpIds));
+        k_push_write<<<cdiv(nA, 256), 256, 0, s>>>(nA, begin1, tc, P<unsigned>(h->caKeysS), kb, gn,
+                                                   P<int>(h->cpOff), P<unsigned>(h->cpKeys), P<int>(h->cpIds));
         if ((rc = sort_pairs(h, P<unsigned>(h->cpKeys), P<unsigned>(h->cpKeysS), P<int>(h->cpIds), P<int>(h->cpIdsS),
-                             nP, B, s, "push sort")))
+                             nP, Bk, s, "push sort")))
             return rc;
         // .cpp:1236-1252: diag(target) += additional[x], x ascending (row-major rows)
         k_fold_runs<DenseDiag, false, unsigned><<<cdiv(nP, 64), 64, 0, s>>>(
-            nP, 0xffffffffu, P<unsigned>(h->cpKeysS), P<int>(h->cpIdsS), P<float>(h->additional), DenseDiag{dense});
+            nP, 0xffffffffu, P<unsigned>(h->cpKeysS), P<int>(h->cpIdsS), P<float>(h->additional),
+            DenseDiag{dense, kb});
     }
     return hip_check(h, hipGetLastError(), "contact kernels");
 }
@@ -1278,12 +1329,12 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     h->denseFine = !fused || h->cfg.keep_blocks;
     const int nStored = h->denseFine ? h->nBlk : h->nBlk - h->nFineBlk;
     const size_t denseBytes = (size_t)std::max(nStored, 1) * kDenseFloats * 4;
-    if (h->earlyFused && h->inv.bytes < (size_t)h->nBlk * kBlockFloats * 4) {
+    if (h->earlyPlanned && h->inv.bytes < (size_t)h->nBlk * kBlockFloats * 4) {
         // the fused kernel is writing the level-0 inverses into inv: let it
         // finish, then grow inv keeping them (first Prepare of a hierarchy
         // with more coarse blocks than run_level0_early reserved)
         Buffer grown;
-        if ((rc = hip_check(h, hipStreamSynchronize(h->prepStream), "prepare stream")) ||
+        if ((rc = finish_early(h)) || (rc = hip_check(h, hipStreamSynchronize(h->prepStream), "prepare stream")) ||
             (rc = hip_check(h, hipMalloc(&grown.p, (size_t)h->nBlk * kBlockFloats * 4), "hipMalloc inv")))
             return rc;
         grown.bytes = (size_t)h->nBlk * kBlockFloats * 4;
@@ -1306,7 +1357,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
          (rc = hip_check(h, hipMemsetAsync(static_cast<char*>(h->dense.p) + zeroFrom, 0, coarseBytes, s),
                          "memset dense"))) ||
         (rc = hip_check(h, hipMemsetAsync(h->additional.p, 0, (size_t)(tc + 1) * 36, s), "memset additional")) ||
-        (!h->odDone && (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt"))))
+        (!(h->earlyPlanned && h->earlyOd) &&  // else od / record counts come from the early path
+         (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt"))))
         return rc;
     float* dense = dense_base(h);
     float* add = P<float>(h->additional);
@@ -1314,13 +1366,15 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     FineContacts fc{};
     // level-0 additional rows: add0 when run_level0_early built them
     FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges,
-               h->earlyFused ? P<float>(h->add0) : add, nullptr, nullptr, nullptr, nullptr,
+               h->earlyPlanned ? P<float>(h->add0) : add, nullptr, nullptr, nullptr, nullptr,
                h->cfg.keep_blocks ? dense : nullptr};
     bool forked = false;
     if (h->nStencil && (rc = run_contacts(h, s, fc, fa, forked))) return rc;
     if (fused) {
         // the level-0 blocks assemble and factor on prepStream while this
-        // stream assembles the coarse levels (run_factor joins)
+        // stream assembles the coarse levels (run_factor joins); the early
+        // path's worker has queued its part by now (its state is read below)
+        if ((rc = finish_early(h))) return rc;
         if (h->earlyFused) {
             // add0 (and od, earlyOd) from the early path (run_level0_early)
             if ((rc = hip_check(h, hipStreamWaitEvent(s, h->evAdd0, 0), "wait add0"))) return rc;

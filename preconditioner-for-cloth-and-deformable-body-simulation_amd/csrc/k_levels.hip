@@ -490,7 +490,7 @@ static int build_levels(mas_context* h, hipStream_t s, const std::function<int()
     }
     h->totalClusters = h->levelSize[2 * L + 1];  // TotalNodes, .cpp:1086-1090
     h->nBlk = h->totalClusters / 32;
-    h->nFineBlk = nv32 / 32;
+    // (set by run_prepare before the early path forked; its worker reads it)
     k_vertex_maps<<<g, 256, 0, s>>>(nV, L, P<int>(h->s2o), gn, P<int4>(h->coarseTables), P<int4>(h->vmap));
     return hip_check(h, hipGetLastError(), "level kernels");
 }
@@ -574,7 +574,7 @@ int run_levels(mas_context* h, hipStream_t s, const int* d_ranges, const std::fu
         std::copy(h->meshLevelSize, h->meshLevelSize + 18, h->levelSize);
         h->totalClusters = h->levelSize[2 * L + 1];
         h->nBlk = h->totalClusters / 32;
-        h->nFineBlk = nv32 / 32;
+        // nFineBlk: set by run_prepare before the early path forked (its worker reads it)
         h->hierId = h->meshHierId;
         h->lastHierDirty = L;
         return MAS_OK;

@@ -233,6 +233,12 @@ struct mas_context {
     int fusedAfterLevels = 0;  // A/B (env MAS_FUSED_AFTER_LEVELS): the early fused kernel waits for the level build
     int earlyThread = 1;       // the early path queued from a second host thread (env MAS_EARLY_THREAD)
     std::unique_ptr<mas::PrepWorker> prepWorker;  // that thread (created by the first Prepare that needs it)
+    // this Prepare runs the early path (decided before it is queued, so the
+    // caller's thread need not wait for the worker to know it); the worker's
+    // job is in flight until finish_early(), which returns its status
+    bool earlyPlanned = false, earlyPending = false;
+    int earlyRc = 0;
+    std::string earlyErr;
     int earlyOd = 0;           // A/B (env MAS_EARLY_OD): k_od in the early path
     bool odDone = false;       // this Prepare's od / record counts are queued already
     mas::FineAsm earlyFa{};    // its inputs, kept for launch_level0_fused
@@ -401,6 +407,8 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
 // the early fused kernel itself, when it waits for the level build (fusedAfterLevels)
 int launch_level0_fused(mas_context* h, hipStream_t s);
 bool early_fused_wanted(const mas_context* h);
+// waits for the early path's worker job (if one is in flight) and returns its status
+int finish_early(mas_context* h);
 int prep_stream_init(mas_context* h);  // prepStream (CU-masked) and its events
 int run_factor(mas_context* h, hipStream_t s);
 // fused level-0 assemble + factor of blocks [blk0, blk1) (k_factor.hip)

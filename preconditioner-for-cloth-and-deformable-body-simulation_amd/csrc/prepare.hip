@@ -6,6 +6,13 @@ namespace mas {
 
 int prepare_apply_tables(mas_context* h, hipStream_t s);
 
+int finish_early(mas_context* h) {
+    if (!h->earlyPending) return MAS_OK;
+    h->prepWorker->wait();
+    h->earlyPending = false;
+    return h->earlyRc ? fail(h, h->earlyRc, h->earlyErr) : MAS_OK;
+}
+
 int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, const void* ef,
                 const void* ee, const void* vf, const unsigned* efC, const unsigned* eeC, const unsigned* vfC,
                 hipStream_t s) {
@@ -33,39 +40,46 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     h->earlyFused = false;
     h->nBlkPrev = h->nBlk;
     const bool early = early_fused_wanted(h);
+    h->earlyPlanned = early;
     if (early && ((rc = prep_stream_init(h)) || (rc = hip_check(h, hipEventRecord(h->evPrepFork, s), "fork"))))
         return rc;
+    // the worker's job never outlives this call, whatever path returns
+    struct JoinEarly {
+        mas_context* h;
+        ~JoinEarly() { finish_early(h); }
+    } joinEarly{h};
     if (early && h->earlyThread) {
         // a second host thread queues prepStream's work while this one queues
-        // the level build: each stream is fed from the start (one thread
-        // queueing both left the early path behind the level kernels): the
-        // handle's PrepWorker, which selects the handle's device first
-        // (ensure() allocates on the current device).  Its error message is
-        // stored by this thread after the wait.
-        int earlyRc = MAS_OK;
-        std::string earlyErr;
+        // the level build and the coarse assembly: each stream is fed from
+        // the start (one thread queueing both left the early path behind the
+        // level kernels): the handle's PrepWorker, which selects the handle's
+        // device first (ensure() allocates on the current device).  This
+        // thread waits for it only where it needs the early path's state
+        // (finish_early in run_assemble): waiting right after the level build
+        // kept the coarse assembly ~300 us behind the worker's ~40 launches.
         if (!h->prepWorker) h->prepWorker = std::make_unique<PrepWorker>(h->device);
-        h->prepWorker->post([&](bool devOk) {
+        h->earlyRc = MAS_OK;
+        h->earlyErr.clear();
+        h->earlyPending = true;
+        h->prepWorker->post([h, d_diag9, d_off9, d_ranges, s](bool devOk) {
             if (!devOk) {
-                earlyRc = MAS_ERR_HIP;
-                earlyErr = "early Prepare thread: hipSetDevice failed";
+                h->earlyRc = MAS_ERR_HIP;
+                h->earlyErr = "early Prepare thread: hipSetDevice failed";
                 return;
             }
-            ErrorSink sink(&earlyErr);  // fail() from this thread writes earlyErr, not h->err
-            earlyRc = run_level0_early(h, d_diag9, d_off9, d_ranges, s);
+            ErrorSink sink(&h->earlyErr);  // fail() from this thread writes earlyErr, not h->err
+            h->earlyRc = run_level0_early(h, d_diag9, d_off9, d_ranges, s);
         });
-        rc = run_levels(h, s, d_ranges);
-        h->prepWorker->wait();
-        if (rc) return rc;
-        if (earlyRc) return fail(h, earlyRc, earlyErr);
+        if ((rc = run_levels(h, s, d_ranges))) return rc;
     } else if ((rc = run_levels(h, s, d_ranges, [&]() {
                     return early ? run_level0_early(h, d_diag9, d_off9, d_ranges, s) : MAS_OK;
                 }))) {
         return rc;
     }
-    if (h->earlyFused && h->fusedAfterLevels && (rc = launch_level0_fused(h, s))) return rc;
+    if (h->fusedAfterLevels && ((rc = finish_early(h)) || (h->earlyFused && (rc = launch_level0_fused(h, s)))))
+        return rc;
     hipEventRecord(e0, s);
-    if ((rc = run_assemble(h, d_diag9, d_off9, d_ranges, s))) return rc;
+    if ((rc = run_assemble(h, d_diag9, d_off9, d_ranges, s)) || (rc = finish_early(h))) return rc;
     hipEventRecord(e1, s);
     if ((rc = run_factor(h, s))) return rc;
     const int nCoarseNodes = h->totalClusters - h->levelSize[3];

@@ -13,7 +13,9 @@ cfg_name = sys.argv[1] if len(sys.argv) > 1 else "1M+contacts"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 mesh, cfg = meshgen.build_config(cfg_name)
 contacts = meshgen.vf_contacts(mesh, cfg["contacts"], seed=3) if cfg["contacts"] else None
-P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts)
+# PREP_SHARD=rank,world: a sharded Prepare (mas_set_prepare_shard) of that rank
+shard = tuple(int(x) for x in os.environ["PREP_SHARD"].split(",")) if os.environ.get("PREP_SHARD") else None
+P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts, shard=shard)
 for _ in range(reps):
     t0 = time.perf_counter()
     if contacts is None:

@@ -28,19 +28,23 @@ def prep(P):
 def line(tag, st):
     return (f"{tag}: prepare {st['prepare_ms']:.3f} ms (levels {st['prepare_levels_ms']:.3f}, assemble "
             f"{st['prepare_assemble_ms']:.3f}, factor {st['prepare_factor_ms']:.3f}, "
-            f"fused level-0 {st['prepare_fine_ms']:.3f})")
+            f"fused level-0 {st['prepare_fine_ms']:.3f} from {st['prepare_fine_start_ms']:.3f}, "
+            f"hier rebuilt {st['hier_rebuilt']})")
 
 
-handles = [("unsharded", mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts))]
-handles += [(f"rank {g}/{world}", mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts,
-                                                     shard=(g, world))) for g in range(world)]
+# one handle at a time (created, measured, destroyed): every handle owns two
+# or three HIP streams, and with more streams alive than GPU_MAX_HW_QUEUES
+# (4) they share hardware queues, which would serialise a Prepare's overlap
+tags = ["unsharded"] + [f"rank {g}/{world}" for g in range(world)]
 best = {}
-for _ in range(reps):
-    for tag, P in handles:
+for i, tag in enumerate(tags):
+    P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts,
+                          shard=None if i == 0 else (i - 1, world))
+    for _ in range(reps):
         st = prep(P)
         if tag not in best or st["prepare_ms"] < best[tag]["prepare_ms"]:
             best[tag] = st
-for tag, _ in handles:
+    del P
     print(line(tag, best[tag]), flush=True)
-slow = max(best[t]["prepare_ms"] for t, _ in handles[1:])
+slow = max(best[t]["prepare_ms"] for t in tags[1:])
 print(f"{cfg_name} world {world}: slowest rank {slow:.3f} ms = {slow / best['unsharded']['prepare_ms']:.3f} x unsharded")
