@@ -59,3 +59,24 @@ def test_mfma_z_within_tolerance_1m_contacts(variant, monkeypatch):
     err = float(np.linalg.norm((z - zo)[:, :3]) / np.linalg.norm(zo[:, :3]))
     print(f"1M + contacts, MFMA formation: z rel. error vs oracle {err:.2e}")
     assert err <= 1e-5, err
+
+
+def test_default_formation_blocks_256k():
+    """The library default (matrix-core formation inside the fused level-0
+    kernel) against the reference-order formation (mas_config
+    .reference_formation = 1) block by block at BASELINE configs[1] (256k
+    cloth, 3 levels): every 8th level-0 block and every coarse block within
+    2e-5 relative (Frobenius)."""
+    import mas_amd
+    mesh = cloth(512)
+    Pd = mas_amd.from_mesh(mesh, max_levels=3)
+    Pr = mas_amd.from_mesh(mesh, max_levels=3, reference_formation=True)
+    assert Pd.stats()["factor_formation"] == 1 and Pr.stats()["factor_formation"] == 0
+    info = Pd.info()
+    blocks = list(range(0, info["num_fine_blocks"], 8)) + list(range(info["num_fine_blocks"], info["num_blocks"]))
+    worst = 0.0
+    for blk in blocks:
+        a, b = Pr.block_inverse(blk), Pd.block_inverse(blk)
+        worst = max(worst, float(np.linalg.norm(b - a) / max(np.linalg.norm(a), 1e-30)))
+    print(f"256k: {len(blocks)} blocks, worst inverse rel. difference {worst:.2e}")
+    assert worst <= 2e-5, worst
