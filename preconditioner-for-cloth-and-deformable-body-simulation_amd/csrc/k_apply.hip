@@ -1,9 +1,10 @@
 // k_apply.hip -- Preconditioning (.cpp:100-110, 1548-1719): the hot path.
 //
 // Per apply, on one stream: the coarse levels, then k_solve_fine.  For
-// L >= 3 the coarse levels default to two launches (k_coarse.hip: the
-// restrictions, then every solve); the per-level form below is kept as
-// coarseMode 0 (and is the L = 2 path).  Both forms are bitwise equal.
+// L >= 3 the coarse levels default to one launch (k_coarse1.hip; the
+// two-launch form k_coarse.hip is taken while a graph is captured); the
+// per-level form below is kept as coarseMode 0 (and is the L = 2 path).  All
+// forms are bitwise equal.
 //   k_coarse_l1         per level-1 block (one wave): R1 of its 32 nodes from
 //                       r gathered through the Morton map, summed per parent
 //                       in lane order from +0 exactly as the reference's owner
@@ -42,19 +43,29 @@ static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThread
 // and emit this workgroup's r.z (fp64; a fixed xor butterfly per wave, then
 // the waves in order) to rzPart[blockIdx.x], so the solver needs no separate
 // pass over r and z.
+// VAR 4 (A/B, MAS_FINE_VARIANT=4): nontemporal, and workgroups are dealt to
+// the XCDs in contiguous chunks (workgroup g runs on XCD g % 8, so logical
+// workgroup (g % 8) * (G / 8) + g / 8): Morton-adjacent blocks then share an
+// XCD's L2 for the r lines they gather and the z lines they write.
+__device__ __forceinline__ int xcd_chunked(int g, int G) {
+    const int full = G & ~7;
+    return g < full ? (g & 7) * (full >> 3) + (g >> 3) : g;
+}
+
 template <int NPROL, int VAR, bool RZ, int WPB = kApplyThreads / 64>
 __device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, int blk0, int nFineBlk, int nV,
                                                 const float4* __restrict__ r, const int4* __restrict__ vmap,
                                                 const float4* __restrict__ zc, int begin1, float4* __restrict__ z,
                                                 double* __restrict__ rzPart) {
     const int lane = threadIdx.x & 63, n = lane & 31;
-    const int blk = blk0 + blockIdx.x * WPB + (threadIdx.x >> 6);
+    const int wg = VAR == 4 ? xcd_chunked(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int blk = blk0 + wg * WPB + (threadIdx.x >> 6);
     const bool bvalid = blk < nFineBlk;
     const int v = blk * 32 + n;
     const bool vvalid = bvalid && v < nV;
     const int4 m = vmap[vvalid ? v : 0];
     float g[kRecord], tl[3];
-    load_record<VAR == 1>(inv, bvalid ? blk : 0, lane, g, tl);
+    load_record<VAR != 0>(inv, bvalid ? blk : 0, lane, g, tl);
     const float4 rv = r[m.x];
     const float3 rr = vvalid ? make_float3(rv.x, rv.y, rv.z) : make_float3(0.f, 0.f, 0.f);
     float3 out = block_solve(g, tl, rr, lane);
@@ -259,6 +270,9 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
                                                                        done, rzPart);
     } else if (var == 3) {
         k_solve_fine1<NPROL><<<blkEnd - blk0, 64, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
+    } else if (var == 4) {
+        k_solve_fine<NPROL, 4, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
+                                                                    nullptr, nullptr);
     } else if (var == 0) {
         k_solve_fine<NPROL, 0, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                     nullptr, nullptr);

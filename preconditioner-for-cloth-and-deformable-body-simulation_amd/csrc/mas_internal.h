@@ -193,7 +193,7 @@ struct mas_context {
     int coarseNarrow = -1;  // single-wave coarse workgroups: -1 = at L = 3, 0 = never, 1 = always (env MAS_COARSE_NARROW)
     // fine kernel (env MAS_FINE_VARIANT, k_apply.hip): 1 = nontemporal inverse
     // loads (4-wave workgroups); 3 = the same in one-wave workgroups (A/B);
-    // 0 = default-policy loads (A/B)
+    // 0 = default-policy loads (A/B); 4 = 1 with XCD-chunked workgroups (A/B)
     int fineVariant = 1;
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     int nStencilEF = 0;  // of nStencil, the EF stencils (at most 5 vertices; EE / VF have 4)
