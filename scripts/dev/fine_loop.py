@@ -7,13 +7,25 @@ per-phase averages of K profiled applies (mas_stats)."""
 import json, os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..",
                                 "preconditioner-for-cloth-and-deformable-body-simulation_amd", "python"))
+import numpy as np
 import torch
 import mas_amd
 from mas_amd import meshgen
 
 cfgname = sys.argv[1] if len(sys.argv) > 1 else "1M+contacts"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-mesh, cfg = meshgen.build_config(cfgname)
+# the mesh is cached under /tmp across the processes of one GPU call (the 4M
+# tet takes ~40 s to generate on the host)
+cache = f"/tmp/mas_mesh_{cfgname}.npz"
+if os.path.exists(cache):
+    f = np.load(cache)
+    mesh, cfg = meshgen.Mesh(*(f[k] for k in ("pos", "starts", "idx", "diag", "off", "faces", "edges"))), \
+        meshgen.CONFIGS[cfgname]
+else:
+    mesh, cfg = meshgen.build_config(cfgname)
+    np.savez(cache + ".part.npz", pos=mesh.pos, starts=mesh.starts, idx=mesh.idx, diag=mesh.diag, off=mesh.off,
+             faces=mesh.faces, edges=mesh.edges)
+    os.replace(cache + ".part.npz", cache)
 contacts = meshgen.vf_contacts(mesh, cfg["contacts"], seed=3) if cfg["contacts"] else None
 P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts, device=0)
 r = torch.from_numpy(meshgen.residual(mesh.nV, 0x5EED)).cuda()

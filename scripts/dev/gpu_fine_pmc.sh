@@ -13,7 +13,7 @@ P5="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_EA0_RDREQ_32B_sum 
 cd $R && timeout -k 10 400 python3 scripts/ab_fine.py 1,3,4 4M-tet > $O/ab_4M.json 2> $O/ab_4M.err && \
 timeout -k 10 200 python3 scripts/ab_fine.py 1,3,4 1M+contacts > $O/ab_1M.json 2> $O/ab_1M.err && \
 cd /tmp && \
-for cv in 1M+contacts:1 4M-tet:1 4M-tet:3 4M-tet:4; do cfg=${cv%:*}; v=${cv#*:}; t=${cfg%%+*}_v$v; \
+for cv in 1M+contacts:1 4M-tet:1 4M-tet:3; do cfg=${cv%:*}; v=${cv#*:}; t=${cfg%%+*}_v$v; \
   MAS_FINE_VARIANT=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$t/trace -o run --output-format csv -- python3 $R/scripts/dev/fine_loop.py $cfg 20 > $O/$t.trace.log 2>&1 && \
   MAS_FINE_VARIANT=$v timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/$t/p1 -o run --output-format csv -- python3 $R/scripts/dev/fine_loop.py $cfg 10 > $O/$t.p1.log 2>&1 && \
   MAS_FINE_VARIANT=$v timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/$t/p2 -o run --output-format csv -- python3 $R/scripts/dev/fine_loop.py $cfg 10 > $O/$t.p2.log 2>&1 && \
