@@ -38,15 +38,18 @@ static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThread
 // The packed inverses are read exactly once per apply (630 MB at 1M, more
 // than the 256 MiB Infinity Cache), so they are loaded nontemporal: measured
 // 98.8 vs 109.7 us per launch at 1M against default-policy loads (VAR = 0,
-// env MAS_FINE_VARIANT=0 keeps that variant for A/B runs).
+// env MAS_FINE_VARIANT=0 keeps that variant for A/B runs; VAR = 1: the
+// nontemporal form without the XCD chunking of VAR = 4).
 // RZ (the PCG driver's applies, k_pcg.hip): exit at once when *done is set,
 // and emit this workgroup's r.z (fp64; a fixed xor butterfly per wave, then
 // the waves in order) to rzPart[blockIdx.x], so the solver needs no separate
 // pass over r and z.
-// VAR 4 (A/B, MAS_FINE_VARIANT=4): nontemporal, and workgroups are dealt to
-// the XCDs in contiguous chunks (workgroup g runs on XCD g % 8, so logical
-// workgroup (g % 8) * (G / 8) + g / 8): Morton-adjacent blocks then share an
-// XCD's L2 for the r lines they gather and the z lines they write.
+// VAR 4 (the default, MAS_FINE_VARIANT=4): nontemporal, and workgroups are
+// dealt to the XCDs in contiguous chunks (workgroup g runs on XCD g % 8, so
+// logical workgroup (g % 8) * (G / 8) + g / 8): Morton-adjacent blocks then
+// share an XCD's L2 for the r lines they gather and the z lines they write.
+// Interleaved in one process, bitwise equal (profiles/round4/fine_pmc/ab_*.json):
+// 4M tet 382 -> 357 us per launch, 1M + contacts 98.5 -> 98.0 us.
 __device__ __forceinline__ int xcd_chunked(int g, int G) {
     const int full = G & ~7;
     return g < full ? (g & 7) * (full >> 3) + (g >> 3) : g;
@@ -264,6 +267,9 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
     if (rzPart) {  // the PCG driver's applies
         if (var == 0)
             k_solve_fine<NPROL, 0, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
+                                                                       done, rzPart);
+        else if (var == 4)
+            k_solve_fine<NPROL, 4, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                        done, rzPart);
         else
             k_solve_fine<NPROL, 1, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
