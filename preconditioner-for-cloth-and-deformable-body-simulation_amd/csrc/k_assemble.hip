@@ -1208,6 +1208,9 @@ static void launch_od(mas_context* h, const FineAsm& fa, hipStream_t s) {
     else k_od<<<cdiv(nV, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
 }
 
+// od and the record counts in the early path (see run_level0_early)
+static bool early_od(const mas_context* h) { return h->earlyOd > 0 || (h->earlyOd < 0 && h->prepWorld > 1); }
+
 bool early_fused_wanted(const mas_context* h) {
     const int nv32 = h->nFineBlk * 32;
     return h->factorVariant >= 4 && !h->cfg.keep_blocks && nv32 > 0 &&
@@ -1285,12 +1288,15 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
         fa.cent = P<int>(h->c0Ent);
         fa.cvals = P<float>(h->c0Val);
     }
-    // earlyOd (A/B, env MAS_EARLY_OD): od and the record counts need only
-    // level-0 data too and can run here, ahead of the fused kernel, instead of
-    // on the caller's reserved CUs -- which delays the fused kernel, most
-    // often the longer path with 64 CUs reserved
+    // earlyOd (env MAS_EARLY_OD; default for a sharded Prepare): od and the
+    // record counts need only level-0 data too and can run here, ahead of the
+    // fused kernel, instead of on the caller's reserved CUs.  Unsharded that
+    // delays the fused kernel, the longer path; a shard's fused kernel is 1/world
+    // of the blocks and the replicated coarse chain is the longer path, which
+    // then no longer carries od: world-8 rank at 1M + contacts 1.40-1.43 ->
+    // 1.37-1.39 ms (profiles/round4/prepare/shard_sweep/)
     h->odDone = false;
-    if (h->earlyOd) {
+    if (early_od(h)) {
         if ((rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
             (rc = hip_check(h, hipMemsetAsync(P<int>(h->recCnt) + nV, 0, 4, ps), "memset recCnt")))
             return rc;
@@ -1357,7 +1363,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
          (rc = hip_check(h, hipMemsetAsync(static_cast<char*>(h->dense.p) + zeroFrom, 0, coarseBytes, s),
                          "memset dense"))) ||
         (rc = hip_check(h, hipMemsetAsync(h->additional.p, 0, (size_t)(tc + 1) * 36, s), "memset additional")) ||
-        (!(h->earlyPlanned && h->earlyOd) &&  // else od / record counts come from the early path
+        (!(h->earlyPlanned && early_od(h)) &&  // else od / record counts come from the early path
          (rc = hip_check(h, hipMemsetAsync(h->recCnt.p, 0, (size_t)(nV + 1) * 4, s), "memset recCnt"))))
         return rc;
     float* dense = dense_base(h);

@@ -273,6 +273,7 @@ __device__ __forceinline__ void fold_wave_grouped(const Coarse1Args& a, int T) {
     const int lane = threadIdx.x & 63, j = lane & 31;
     const int2 mb = a.members[a.lv3Begin + T - a.begin1];  // (level-2 bank, children)
     const bool child = lane < 32 && (((unsigned)mb.y >> j) & 1u);
+    C1_STAMP(0, T, 0);
     unsigned long long v[3] = {0ull, 0ull, 0ull};
     bool ok = !child;
     for (int d = 0; d < a.pollDelay; ++d) __builtin_amdgcn_s_sleep(64);
@@ -285,6 +286,7 @@ __device__ __forceinline__ void fold_wave_grouped(const Coarse1Args& a, int T) {
         __builtin_amdgcn_s_sleep(1);
     }
     if (!__all(ok) && lane == 0) atomicAdd(a.timeouts, 1);  // R3 from stale R2: counted
+    C1_STAMP(0, T, 1);
     const float x = child ? tag_val(v[0]) : 0.f, y = child ? tag_val(v[1]) : 0.f, z = child ? tag_val(v[2]) : 0.f;
     float ax = 0.f, ay = 0.f, az = 0.f;
 #pragma unroll
@@ -293,10 +295,12 @@ __device__ __forceinline__ void fold_wave_grouped(const Coarse1Args& a, int T) {
         ay = __fadd_rn(ay, __shfl(y, k));
         az = __fadd_rn(az, __shfl(z, k));
     }
+    C1_STAMP(0, T, 2);
     if (lane == 0) {
         st_tag(a.tR3 + T, ax, ay, az, a.epoch);
         a.rc[a.lv3Begin + T - a.begin1] = make_float4(ax, ay, az, 0.f);
     }
+    C1_STAMP(0, T, 3);
 }
 
 // ---------------------------------------------------------------------------

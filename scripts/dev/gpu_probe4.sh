@@ -1,0 +1,16 @@
+# Round 4: sharded Prepare with od in the early path (tests, one rank);
+# in-kernel timeline of the one-launch coarse form (grouped level 3)
+# at 1M + contacts and 4M tet (probe build, lib/libmas_amd_probe.so); then, on
+# the same box, the 4M fine kernel interleaved in one process with three
+# handles (scripts/ab_fine.py) against one handle per process (fine_loop.py).
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-probe4}; mkdir -p $O; export TMPDIR=/tmp
+cd $R && timeout -k 10 400 python -u -m pytest tests/test_gpu_shard.py tests/test_gpu_prepare_paths.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 && \
+PREP_SHARD=3,8 timeout -k 10 200 python3 scripts/dev/prep_only.py 1M+contacts 6 > $O/rank3.log 2>&1 && \
+timeout -k 10 200 python3 scripts/dev/probe_coarse1.py 1M+contacts > $O/probe_1M.txt 2>&1 && \
+timeout -k 10 300 python3 scripts/dev/probe_coarse1.py 4M-tet > $O/probe_4M.txt 2>&1 && \
+timeout -k 10 300 python3 scripts/ab_fine.py 1,4 4M-tet > $O/ab_4M.json 2> $O/ab.err && \
+MAS_FINE_VARIANT=1 timeout -k 10 300 python3 scripts/dev/fine_loop.py 4M-tet 400 > $O/loop_4M_v1.json 2>> $O/ab.err && \
+MAS_FINE_VARIANT=4 timeout -k 10 300 python3 scripts/dev/fine_loop.py 4M-tet 400 > $O/loop_4M_v4.json 2>> $O/ab.err && \
+timeout -k 10 300 python3 scripts/ab_fine.py 4,1 4M-tet > $O/ab_4M_rev.json 2>> $O/ab.err
+echo "exit $?"

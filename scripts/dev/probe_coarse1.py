@@ -32,18 +32,21 @@ lib.mas_probe1_dump(buf.ctypes.data, buf.size)
 buf = buf.reshape(3, 8192, 8).astype(np.int64)
 t0 = buf[buf > 0].min()
 print(name, "levels", P.info()["level_size"].tolist())
-labels = {0: ["start", "first prefix", "fold end", "R3 published"],
+labels = {0: ["start", "first prefix / R2 polled", "fold end", "R3 published"],
           1: ["start", "staged", "R1/R2 published", "Z1 stored"],
           2: ["start", "R polled", "Z stored"]}
-names = {0: "level-3 fold waves", 1: "bank waves", 2: "level-2/3 solve waves"}
-for kind in (0, 1, 2):
-    b = buf[kind]
+names = {0: "level-3 fold waves", 1: "bank waves", 2: "level-2 solve waves", 3: "level-3 solve waves"}
+nb2 = (int(P.info()["level_size"][2][0]) + 31) // 32  # solve-wave slots: level 2 first, then level 3
+for kind in (0, 1, 2, 3):
+    b = buf[min(kind, 2)]
+    if kind >= 2:
+        b = b[:nb2] if kind == 2 else b[nb2:]
     live = b[:, 0] > 0
     if not live.any():
         continue
     b = b[live]
     print(f"{names[kind]}: {len(b)}")
-    for s, lab in enumerate(labels[kind]):
+    for s, lab in enumerate(labels[min(kind, 2)]):
         m = b[:, s] > 0
         if not m.any():
             continue
