@@ -35,6 +35,12 @@ int hip_check(mas_context* h, hipError_t e, const char* what) {
 int ensure(mas_context* h, Buffer& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.bytes >= bytes) return MAS_OK;
+    // every allocation of a handle lives on its device: a thread that forgot
+    // hipSetDevice (the early-path worker selects it per job) fails loudly here
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != h->device)
+        return fail(h, MAS_ERR_STATE, "allocation on device " + std::to_string(dev) + " for a handle of device " +
+                                          std::to_string(h->device));
     if (b.p) {
         hipStreamSynchronize(h->stream);
         hipFree(b.p);

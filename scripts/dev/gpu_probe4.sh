@@ -5,7 +5,7 @@
 # handles (scripts/ab_fine.py) against one handle per process (fine_loop.py).
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-probe4}; mkdir -p $O; export TMPDIR=/tmp
-cd $R && timeout -k 10 400 python -u -m pytest tests/test_gpu_shard.py tests/test_gpu_prepare_paths.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 && \
+cd $R && timeout -k 10 400 python -u -m pytest tests/test_gpu_shard.py tests/test_gpu_prepare_paths.py tests/test_gpu_restrict.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 && \
 PREP_SHARD=3,8 timeout -k 10 200 python3 scripts/dev/prep_only.py 1M+contacts 6 > $O/rank3.log 2>&1 && \
 timeout -k 10 200 python3 scripts/dev/probe_coarse1.py 1M+contacts > $O/probe_1M.txt 2>&1 && \
 timeout -k 10 300 python3 scripts/dev/probe_coarse1.py 4M-tet > $O/probe_4M.txt 2>&1 && \
