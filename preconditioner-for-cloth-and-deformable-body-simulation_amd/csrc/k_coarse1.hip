@@ -102,6 +102,7 @@ struct Coarse1Args {
     unsigned epoch;       // this apply's tag
     int nb1;
     int pollDelay;        // fold / solve waves: s_sleep(64) rounds before the first poll (A/B)
+    int chunk;            // bank waves XCD-chunked (k_apply.hip xcd_chunked; A/B)
     const int* done;      // PCG: exit at once when set
     int pollLimit;        // polls before a wait gives up (kPollLimit; < 0: give up at once, a test knob)
     int* timeouts;        // waits that gave up: this apply's z is incomplete (mas_stats.wait_timeouts)
@@ -340,7 +341,10 @@ __global__ __launch_bounds__(64) void k_coarse1(Coarse1Args a) {
     if (a.done && *a.done) return;
     __shared__ C1Shared sh;
     int w = blockIdx.x;  // workgroup-uniform roles
-    if (w < a.nb1) return bank_wave(a, w, sh);
+    if (w < a.nb1) {  // the first nb1 workgroups: workgroup w runs on XCD w % 8
+        const int full = a.nb1 & ~7;
+        return bank_wave(a, a.chunk && w < full ? (w & 7) * (full >> 3) + (w >> 3) : w, sh);
+    }
     w -= a.nb1;
     if (w < a.n3) return a.members ? fold_wave_grouped(a, w) : fold_wave(a, w, sh);
     w -= a.n3;
@@ -416,6 +420,7 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.tR3 = a.tR2 + ceil32(a.n2);
     a.epoch = h->coarse1Epoch;
     a.pollDelay = h->c1PollDelay;
+    a.chunk = h->c1Chunk;
     a.done = h->applyDone;
     a.pollLimit = h->c1PollLimit;
     a.members = h->groupedR3 && deep ? P<int2>(h->members) : nullptr;

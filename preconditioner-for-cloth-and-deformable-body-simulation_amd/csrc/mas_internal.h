@@ -291,6 +291,7 @@ struct mas_context {
     mas::Buffer c1Tags, l1info;
     unsigned coarse1Epoch = 0;
     int c1PollDelay = 0;  // A/B (env MAS_C1_POLL_DELAY): fold / solve waves sleep before their first poll
+    int c1Chunk = 0;      // A/B (env MAS_C1_CHUNK): bank waves dealt to the XCDs in contiguous chunks
     // k_coarse1's bounded waits never hang the device: a wait gives up after
     // this many polls and is counted (env MAS_C1_POLL_LIMIT; < 0 forces it: tests)
     int c1PollLimit = 1 << 16;

@@ -12,5 +12,7 @@ timeout -k 10 300 python3 scripts/dev/probe_coarse1.py 4M-tet > $O/probe_4M.txt 
 timeout -k 10 300 python3 scripts/ab_fine.py 1,4 4M-tet > $O/ab_4M.json 2> $O/ab.err && \
 MAS_FINE_VARIANT=1 timeout -k 10 300 python3 scripts/dev/fine_loop.py 4M-tet 400 > $O/loop_4M_v1.json 2>> $O/ab.err && \
 MAS_FINE_VARIANT=4 timeout -k 10 300 python3 scripts/dev/fine_loop.py 4M-tet 400 > $O/loop_4M_v4.json 2>> $O/ab.err && \
-timeout -k 10 300 python3 scripts/ab_fine.py 4,1 4M-tet > $O/ab_4M_rev.json 2>> $O/ab.err
+timeout -k 10 300 python3 scripts/ab_fine.py 4,1 4M-tet > $O/ab_4M_rev.json 2>> $O/ab.err && \
+timeout -k 10 300 python3 scripts/ab_env.py MAS_C1_CHUNK=0 MAS_C1_CHUNK=1 --config 1M+contacts > $O/ab_c1chunk_1M.json 2>> $O/ab.err && \
+timeout -k 10 400 python3 scripts/ab_env.py MAS_C1_CHUNK=0 MAS_C1_CHUNK=1 --config 4M-tet > $O/ab_c1chunk_4M.json 2>> $O/ab.err
 echo "exit $?"
