@@ -9,7 +9,7 @@ O=$R/gpurun_out/${1:-profile}
 mkdir -p $O
 export TMPDIR=/tmp
 cd $R && \
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err && \
 cd /tmp && \
