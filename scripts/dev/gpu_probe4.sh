@@ -14,5 +14,7 @@ MAS_FINE_VARIANT=1 timeout -k 10 300 python3 scripts/dev/fine_loop.py 4M-tet 400
 MAS_FINE_VARIANT=4 timeout -k 10 300 python3 scripts/dev/fine_loop.py 4M-tet 400 > $O/loop_4M_v4.json 2>> $O/ab.err && \
 timeout -k 10 300 python3 scripts/ab_fine.py 4,1 4M-tet > $O/ab_4M_rev.json 2>> $O/ab.err && \
 timeout -k 10 300 python3 scripts/ab_env.py MAS_C1_CHUNK=0 MAS_C1_CHUNK=1 --config 1M+contacts > $O/ab_c1chunk_1M.json 2>> $O/ab.err && \
-timeout -k 10 400 python3 scripts/ab_env.py MAS_C1_CHUNK=0 MAS_C1_CHUNK=1 --config 4M-tet > $O/ab_c1chunk_4M.json 2>> $O/ab.err
+timeout -k 10 400 python3 scripts/ab_env.py MAS_C1_CHUNK=0 MAS_C1_CHUNK=1 --config 4M-tet > $O/ab_c1chunk_4M.json 2>> $O/ab.err && \
+cd /tmp && MAS_FINE_VARIANT=4 timeout -s KILL 300 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_REQ_LATENCY_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum GRBM_GUI_ACTIVE GRBM_UTCL2_BUSY -d $O/4M-tet_v4/p3 -o run --output-format csv -- python3 $R/scripts/dev/fine_loop.py 4M-tet 10 > $O/4M-tet_v4.p3.log 2>&1 && \
+MAS_FINE_VARIANT=4 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/4M-tet_v4/p1 -o run --output-format csv -- python3 $R/scripts/dev/fine_loop.py 4M-tet 10 > $O/4M-tet_v4.p1.log 2>&1
 echo "exit $?"
