@@ -102,7 +102,7 @@ struct Coarse1Args {
     unsigned epoch;       // this apply's tag
     int nb1;
     int pollDelay;        // fold / solve waves: s_sleep(64) rounds before the first poll (A/B)
-    int chunk;            // bank waves XCD-chunked (k_apply.hip xcd_chunked; A/B)
+    int chunk;            // bank waves XCD-chunked (as k_apply.hip xcd_chunked): Morton-adjacent banks share an L2
     const int* done;      // PCG: exit at once when set
     int pollLimit;        // polls before a wait gives up (kPollLimit; < 0: give up at once, a test knob)
     int* timeouts;        // waits that gave up: this apply's z is incomplete (mas_stats.wait_timeouts)

@@ -291,7 +291,11 @@ struct mas_context {
     mas::Buffer c1Tags, l1info;
     unsigned coarse1Epoch = 0;
     int c1PollDelay = 0;  // A/B (env MAS_C1_POLL_DELAY): fold / solve waves sleep before their first poll
-    int c1Chunk = 0;      // A/B (env MAS_C1_CHUNK): bank waves dealt to the XCDs in contiguous chunks
+    // bank waves of the one-launch coarse form dealt to the XCDs in contiguous
+    // chunks (env MAS_C1_CHUNK=0: round-robin, A/B): interleaved, bitwise equal,
+    // pre-fine 14.65 -> 13.82 us at 1M + contacts, 47.5 -> 42.5 us at 4M tet
+    // (profiles/round4/ab/c1chunk_*.json)
+    int c1Chunk = 1;
     // k_coarse1's bounded waits never hang the device: a wait gives up after
     // this many polls and is counted (env MAS_C1_POLL_LIMIT; < 0 forces it: tests)
     int c1PollLimit = 1 << 16;
