@@ -1209,7 +1209,7 @@ static void launch_od(mas_context* h, const FineAsm& fa, hipStream_t s) {
 }
 
 // od and the record counts in the early path (see run_level0_early)
-static bool early_od(const mas_context* h) { return h->earlyOd > 0 || (h->earlyOd < 0 && h->prepWorld > 1); }
+bool early_od(const mas_context* h) { return h->earlyOd > 0 || (h->earlyOd < 0 && h->prepWorld > 1); }
 
 bool early_fused_wanted(const mas_context* h) {
     const int nv32 = h->nFineBlk * 32;
@@ -1370,9 +1370,10 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     float* add = P<float>(h->additional);
     const int* gn = P<int>(h->goingNext);
     FineContacts fc{};
-    // level-0 additional rows: add0 when run_level0_early built them
+    // level-0 additional rows: add0 when run_level0_early built them (its
+    // pointer is read only after the worker is joined: the worker allocates it)
     FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges,
-               h->earlyPlanned ? P<float>(h->add0) : add, nullptr, nullptr, nullptr, nullptr,
+               h->earlyPlanned ? nullptr : add, nullptr, nullptr, nullptr, nullptr,
                h->cfg.keep_blocks ? dense : nullptr};
     bool forked = false;
     if (h->nStencil && (rc = run_contacts(h, s, fc, fa, forked))) return rc;
@@ -1381,6 +1382,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         // stream assembles the coarse levels (run_factor joins); the early
         // path's worker has queued its part by now (its state is read below)
         if ((rc = finish_early(h))) return rc;
+        if (h->earlyPlanned) fa.additional = P<float>(h->add0);
         if (h->earlyFused) {
             // add0 (and od, earlyOd) from the early path (run_level0_early)
             if ((rc = hip_check(h, hipStreamWaitEvent(s, h->evAdd0, 0), "wait add0"))) return rc;
