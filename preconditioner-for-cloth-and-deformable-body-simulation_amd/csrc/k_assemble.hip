@@ -1217,6 +1217,23 @@ bool early_fused_wanted(const mas_context* h) {
            bit_width((unsigned)(nv32 - 1)) + 1 + RecKey::kLaneBits <= 32;  // level-0 keys fit (else the late path)
 }
 
+// The early path's buffers that the caller's thread reads as well, sized by
+// the caller before the worker starts (run_prepare): the level-0 inverses go
+// straight into inv -- room for them now and for a coarse share like the
+// previous Prepare's (run_assemble grows it, keeping the level-0 part, if the
+// hierarchy needs more) -- add0, and od / the record counts when early_od.
+int early_buffers(mas_context* h) {
+    const size_t blockBytes = (size_t)kBlockFloats * 4;
+    const size_t want = (size_t)std::max(h->nBlkPrev, h->nFineBlk + h->nFineBlk / 8 + 64) * blockBytes;
+    int rc;
+    if (h->inv.bytes < (size_t)h->nFineBlk * blockBytes && (rc = ensure(h, h->inv, want))) return rc;
+    if ((rc = ensure(h, h->add0, (size_t)h->nFineBlk * 32 * 36))) return rc;
+    if (early_od(h) && ((rc = ensure(h, h->od, (size_t)h->nV * 36)) ||
+                        (rc = ensure(h, h->recCnt, (size_t)(h->nV + 1) * 4))))
+        return rc;
+    return MAS_OK;
+}
+
 int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, hipStream_t s) {
     h->earlyFused = false;
     if (!early_fused_wanted(h)) return MAS_OK;
@@ -1225,13 +1242,7 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
     static const bool serial = std::getenv("MAS_PREP_SERIAL") && std::atoi(std::getenv("MAS_PREP_SERIAL"));
     hipStream_t ps = serial ? s : h->prepStream;
     const int nV = h->nV, n = h->nStencil, nv32 = h->nFineBlk * 32;
-    // the level-0 inverses go straight into inv: room for them now, and for a
-    // coarse share like the previous Prepare's (run_assemble grows it keeping
-    // the level-0 part if the hierarchy needs more)
-    const size_t blockBytes = (size_t)kBlockFloats * 4;
-    const size_t want = (size_t)std::max(h->nBlkPrev, h->nFineBlk + h->nFineBlk / 8 + 64) * blockBytes;
-    if (h->inv.bytes < (size_t)h->nFineBlk * blockBytes && (rc = ensure(h, h->inv, want))) return rc;
-    if ((rc = ensure(h, h->add0, (size_t)nv32 * 36))) return rc;
+    if ((rc = early_buffers(h))) return rc;  // sized by run_prepare already: no allocation here
     // evPrepFork was recorded on s right after the stencils (run_prepare), before
     // the level kernels: prepStream waits for the stencils only
     if ((rc = hip_check(h, hipStreamWaitEvent(ps, h->evPrepFork, 0), "fork wait")) ||
@@ -1297,9 +1308,7 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
     // 1.37-1.39 ms (profiles/round4/prepare/shard_sweep/)
     h->odDone = false;
     if (early_od(h)) {
-        if ((rc = ensure(h, h->od, (size_t)nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(nV + 1) * 4)) ||
-            (rc = hip_check(h, hipMemsetAsync(P<int>(h->recCnt) + nV, 0, 4, ps), "memset recCnt")))
-            return rc;
+        if ((rc = hip_check(h, hipMemsetAsync(P<int>(h->recCnt) + nV, 0, 4, ps), "memset recCnt"))) return rc;
         launch_od(h, fa, ps);
         h->odDone = true;
     }

@@ -416,6 +416,7 @@ bool early_fused_wanted(const mas_context* h);
 // waits for the early path's worker job (if one is in flight) and returns its status
 int finish_early(mas_context* h);
 bool early_od(const mas_context* h);  // od and the record counts computed by the early path
+int early_buffers(mas_context* h);    // the early path's buffers the caller reads too (run_prepare sizes them)
 int prep_stream_init(mas_context* h);  // prepStream (CU-masked) and its events
 int run_factor(mas_context* h, hipStream_t s);
 // fused level-0 assemble + factor of blocks [blk0, blk1) (k_factor.hip)

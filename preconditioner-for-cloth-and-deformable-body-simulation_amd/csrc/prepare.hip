@@ -43,13 +43,11 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     h->earlyPlanned = early;
     if (early && ((rc = prep_stream_init(h)) || (rc = hip_check(h, hipEventRecord(h->evPrepFork, s), "fork"))))
         return rc;
-    // buffers both threads use (the worker writes od and the record counts,
-    // this thread's coarse assembly reads them) are sized here, before the
-    // worker starts: ensure() on one Buffer from two threads could allocate
-    // it twice and leave them with different pointers
-    if (early && early_od(h) &&
-        ((rc = ensure(h, h->od, (size_t)h->nV * 36)) || (rc = ensure(h, h->recCnt, (size_t)(h->nV + 1) * 4))))
-        return rc;
+    // buffers both threads use (the worker writes inv, add0 and, early_od,
+    // od and the record counts; this thread's assembly reads them) are sized
+    // here, before the worker starts: ensure() on one Buffer from two threads
+    // could allocate it twice and leave them with different pointers
+    if (early && (rc = early_buffers(h))) return rc;
     // the worker's job never outlives this call, whatever path returns
     struct JoinEarly {
         mas_context* h;
