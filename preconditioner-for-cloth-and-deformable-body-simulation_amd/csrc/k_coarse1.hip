@@ -103,7 +103,6 @@ struct Coarse1Args {
     int nb1;
     int pollDelay;        // fold / solve waves: s_sleep(64) rounds before the first poll (A/B)
     int chunk;            // bank waves XCD-chunked (as k_apply.hip xcd_chunked): Morton-adjacent banks share an L2
-    Tag3* tR1b;           // splitZ1: level-1 local id -> R1, polled by the level-1 solve waves; null: banks solve Z1
     const int* done;      // PCG: exit at once when set
     int pollLimit;        // polls before a wait gives up (kPollLimit; < 0: give up at once, a test knob)
     int* timeouts;        // waits that gave up: this apply's z is incomplete (mas_stats.wait_timeouts)
@@ -188,10 +187,6 @@ __device__ __forceinline__ void bank_wave(const Coarse1Args& a, int B, C1Shared&
     }
     if (own) a.rc[c] = make_float4(ax, ay, az, 0.f);
     C1_STAMP(1, B, 2);
-    if (a.tR1b) {  // Z1 by a level-1 solve wave at the end of the grid: this slot frees for the next bank
-        if (own) st_tag(a.tR1b + c, ax, ay, az, a.epoch);
-        return;
-    }
     // Z1 of the bank's block from the R1 in registers (inverse loaded after the
     // publications, so the restriction's gathers do not queue behind it)
     float g[kRecord], tl[3];
@@ -341,7 +336,7 @@ __device__ __forceinline__ void solve_wave(const Coarse1Args& a, int blk, int lv
 }
 
 // grid (single-wave workgroups): [0, nb1) banks, then n3 fold waves, then nb2
-// level-2 and nb3 level-3 solve waves, then (splitZ1) nb1 level-1 solve waves
+// level-2 and nb3 level-3 solve waves
 __global__ __launch_bounds__(64) void k_coarse1(Coarse1Args a) {
     if (a.done && *a.done) return;
     __shared__ C1Shared sh;
@@ -355,9 +350,7 @@ __global__ __launch_bounds__(64) void k_coarse1(Coarse1Args a) {
     w -= a.n3;
     if (w < a.nb2) return solve_wave(a, a.lv2Begin / 32 + w, a.lv2Begin, a.n2, a.tR2, w);
     w -= a.nb2;
-    if (w < a.nb3) return solve_wave(a, a.lv3Begin / 32 + w, a.lv3Begin, a.n3, a.tR3, a.nb2 + w);
-    w -= a.nb3;
-    if (a.tR1b && w < a.nb1) solve_wave(a, a.begin1 / 32 + w, a.begin1, a.n1, a.tR1b, a.nb2 + a.nb3 + w);
+    if (w < a.nb3) solve_wave(a, a.lv3Begin / 32 + w, a.lv3Begin, a.n3, a.tR3, a.nb2 + w);
 }
 
 // per level-1 node: its parent (local to begin1), the parent's child mask, its level-3 list slot
@@ -370,13 +363,12 @@ __global__ __launch_bounds__(256) void k_l1info(int n1, int begin1, const int* _
     info[c] = make_int4(p, members[p].y, deepPos ? deepPos[c] : -1, 0);
 }
 
-// tagged hand-off slots: level-3 lists, then level-2 nodes, then level-3
-// nodes, then level-1 nodes (splitZ1)
+// tagged hand-off slots: level-3 lists, then level-2 nodes, then level-3 nodes
 static size_t coarse1_tags(const mas_context* h) {
     const int n2 = h->levelSize[4];
     const size_t nList = h->L >= 4 ? (size_t)deep_nodes(h) * h->deepStride : 0;
     const size_t n3 = h->L >= 4 ? (size_t)ceil32(h->levelSize[6]) : 0;
-    return nList + ceil32(n2) + n3 + ceil32(h->levelSize[2]);
+    return nList + ceil32(n2) + n3;
 }
 
 int build_coarse1_tables(mas_context* h, hipStream_t s) {
@@ -426,10 +418,6 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.tR1 = t;
     a.tR2 = t + nList;
     a.tR3 = a.tR2 + ceil32(a.n2);
-    // splitZ1 (A/B, env MAS_C1_SPLIT_Z1): the level-1 solves by their own waves
-    // at the end of the grid, so a bank wave's slot frees right after its
-    // restriction (4M: the second round of bank waves starts earlier)
-    a.tR1b = h->c1SplitZ1 ? a.tR3 + (deep ? ceil32(a.n3) : 0) : nullptr;
     a.epoch = h->coarse1Epoch;
     a.pollDelay = h->c1PollDelay;
     a.chunk = h->c1Chunk;
@@ -438,7 +426,7 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.members = h->groupedR3 && deep ? P<int2>(h->members) : nullptr;
     a.timeouts = P<int>(h->devStatus) + 2;
     h->c1Launched = true;
-    k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3 + (a.tR1b ? a.nb1 : 0), 64, 0, s>>>(a);
+    k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3, 64, 0, s>>>(a);
 }
 
 }  // namespace mas

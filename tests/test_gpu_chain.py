@@ -20,16 +20,14 @@ pytestmark = pytest.mark.gpu
 def _handles(mesh, L, contacts, monkeypatch, grouped=False):
     """Per-level (mode 0), two-pass (2), two-pass in its occupancy form
     (SoA restriction staging, no level-3 inverse prefetch), one-launch (3),
-    the wide two-pass form, and one-launch with the level-1 solves in their own
-    waves (MAS_C1_SPLIT_Z1) and with round-robin bank waves (MAS_C1_CHUNK=0)."""
+    the wide two-pass form, and one-launch with round-robin bank waves
+    (MAS_C1_CHUNK=0)."""
     import mas_amd
     hs = []
-    for mode, occ, wide, split, chunk in ((0, 0, 0, 0, 1), (2, 0, 0, 0, 1), (2, 1, 0, 0, 1), (3, 0, 0, 0, 1),
-                                          (2, 0, 1, 0, 1), (3, 0, 0, 1, 1), (3, 0, 0, 0, 0)):
+    for mode, occ, wide, chunk in ((0, 0, 0, 1), (2, 0, 0, 1), (2, 1, 0, 1), (3, 0, 0, 1), (2, 0, 1, 1), (3, 0, 0, 0)):
         monkeypatch.setenv("MAS_COARSE_MODE", str(mode))
         monkeypatch.setenv("MAS_COARSE_OCC", str(occ))
         monkeypatch.setenv("MAS_COARSE_WIDE", str(wide))
-        monkeypatch.setenv("MAS_C1_SPLIT_Z1", str(split))
         monkeypatch.setenv("MAS_C1_CHUNK", str(chunk))
         hs.append(mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, reference_restriction=not grouped))
         assert hs[-1].stats()["apply_mode"] == mode
@@ -58,11 +56,11 @@ def test_twopass_equals_per_level(kind, W, L, nc, grouped, monkeypatch):
     from mas_amd import meshgen
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=11) if nc else None
-    P3, P2, P2o, P1, P2w, P1s, P1r = _handles(mesh, L, contacts, monkeypatch, grouped)
+    P3, P2, P2o, P1, P2w, P1r = _handles(mesh, L, contacts, monkeypatch, grouped)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 100 + k)).cuda() for k in range(24)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    for PX in (P2, P2o, P1, P2w, P1s, P1r):
+    for PX in (P2, P2o, P1, P2w, P1r):
         zf = _applies(PX, rs, s)
         for k, (a, b) in enumerate(zip(zf, z3)):
             np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
@@ -81,11 +79,11 @@ def test_twopass_1m_contacts_bitwise_and_oracle(grouped, monkeypatch):
     from oracle import Oracle
     mesh = cloth(1024)
     contacts = meshgen.vf_contacts(mesh, 100_000, seed=3)
-    P3, P2, P2o, P1, P2w, P1s, P1r = _handles(mesh, 4, contacts, monkeypatch, grouped)
+    P3, P2, P2o, P1, P2w, P1r = _handles(mesh, 4, contacts, monkeypatch, grouped)
     rs = [torch.from_numpy(meshgen.residual(mesh.nV, 0x5EED + k)).cuda() for k in range(40)]
     s = torch.cuda.Stream()
     z3 = _applies(P3, rs, s)
-    for PX in (P2, P2o, P1, P2w, P1s, P1r):
+    for PX in (P2, P2o, P1, P2w, P1r):
         zf = _applies(PX, rs, s)
         for k, (a, b) in enumerate(zip(zf, z3)):
             np.testing.assert_array_equal(a, b, err_msg=f"apply {k}")
