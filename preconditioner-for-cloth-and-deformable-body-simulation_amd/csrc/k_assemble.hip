@@ -1385,19 +1385,6 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                h->earlyPlanned ? nullptr : add, nullptr, nullptr, nullptr, nullptr,
                h->cfg.keep_blocks ? dense : nullptr};
     bool forked = false;
-    // odFirst (A/B, env MAS_OD_FIRST): od and the record counts on this stream
-    // before the coarse contact records, as soon as the early path's add0 is
-    // queued, instead of after them (where they meet the fused kernel on the
-    // reserved CUs)
-    if (fused && h->odFirst && h->earlyPlanned && !early_od(h)) {
-        if ((rc = finish_early(h))) return rc;
-        fa.additional = P<float>(h->add0);
-        if (h->earlyFused) {
-            if ((rc = hip_check(h, hipStreamWaitEvent(s, h->evAdd0, 0), "wait add0"))) return rc;
-            launch_od(h, fa, s);
-            h->odDone = true;
-        }
-    }
     if (h->nStencil && (rc = run_contacts(h, s, fc, fa, forked))) return rc;
     if (fused) {
         // the level-0 blocks assemble and factor on prepStream while this

@@ -242,7 +242,6 @@ struct mas_context {
     std::string earlyErr;
     int earlyOd = -1;          // k_od in the early path: 1 always, 0 never, -1 (default) when the Prepare is sharded
     bool odDone = false;       // this Prepare's od / record counts are queued already
-    int odFirst = 0;           // A/B (env MAS_OD_FIRST): od before the coarse contact records (k_assemble.hip)
     mas::FineAsm earlyFa{};    // its inputs, kept for launch_level0_fused
     hipEvent_t evAdd0 = nullptr;
     mas::Buffer add0, c0Cnt, c0Off, c0Keys, c0KeysS, c0Ids, c0IdsS, c0Val, a0Keys, a0KeysS, a0Ids, a0IdsS, a0Val;
