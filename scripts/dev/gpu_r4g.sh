@@ -1,3 +1,4 @@
+# (lib/libmas_amd_ab_split3.so was a one-off build of 96b66d9 for this A/B; results in profiles/round4/ab/)
 # Round 4: the one-hand-off level-3 wave (solve3_wave) and the deferred
 # early-path join: parity tests, apply A/B against the previous build
 # (lib/libmas_amd_ab_split3.so: fold waves + level-3 solve waves), Prepare

@@ -1,3 +1,4 @@
+# (MAS_C1_SPLIT_Z1 was removed after this measurement: profiles/round4/ab/ab_split_*.json)
 # Round 4: level-1 solves in their own waves (MAS_C1_SPLIT_Z1) -- the coarse
 # forms' bitwise tests, then an interleaved A/B at 1M + contacts, 4M and 256k.
 set -o pipefail
