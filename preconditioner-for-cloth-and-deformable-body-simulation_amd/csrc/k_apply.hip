@@ -123,6 +123,14 @@ __global__ __launch_bounds__(128) void k_solve_fine2(const float4* __restrict__ 
     solve_fine_body<NPROL, 4, false, 2>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, nullptr);
 }
 
+// A/B (MAS_FINE_VARIANT=7): the chunked form in one-wave workgroups.
+template <int NPROL>
+__global__ __launch_bounds__(64) void k_solve_fine1c(const float4* __restrict__ inv, int blk0, int nFineBlk, int nV,
+                                                    const float4* __restrict__ r, const int4* __restrict__ vmap,
+                                                    const float4* __restrict__ zc, int begin1, float4* __restrict__ z) {
+    solve_fine_body<NPROL, 4, false, 1>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, nullptr);
+}
+
 // A/B (MAS_FINE_VARIANT=3): one wave per workgroup.  Measured interleaved,
 // 4M tet: 433.5 -> 394.6 us per launch on one box, 436.3 -> 472.0 us on
 // another; 1M 104.2 -> 107.2 us; 256k unchanged -- not the default.
@@ -290,6 +298,8 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
                                                                     nullptr, nullptr);
     } else if (var == 6) {
         k_solve_fine2<NPROL><<<cdiv(blkEnd - blk0, 2), 128, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
+    } else if (var == 7) {
+        k_solve_fine1c<NPROL><<<blkEnd - blk0, 64, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
     } else if (var == 0) {
         k_solve_fine<NPROL, 0, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                     nullptr, nullptr);
