@@ -44,7 +44,7 @@ static inline int grid_for_blocks(int blocks) { return cdiv(blocks, kApplyThread
 // and emit this workgroup's r.z (fp64; a fixed xor butterfly per wave, then
 // the waves in order) to rzPart[blockIdx.x], so the solver needs no separate
 // pass over r and z.
-// VAR 4 (the default, MAS_FINE_VARIANT=4): nontemporal, and workgroups are
+// VAR 4 (MAS_FINE_VARIANT=4; 6, the default, in two-wave workgroups): nontemporal, and workgroups are
 // dealt to the XCDs in contiguous chunks (workgroup g runs on XCD g % 8, so
 // logical workgroup (g % 8) * (G / 8) + g / 8): Morton-adjacent blocks then
 // share an XCD's L2 for the r lines they gather and the z lines they write.
@@ -91,36 +91,32 @@ __device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, 
     if (RZ) {
         double a = writer ? (double)out.x * rr.x + (double)out.y * rr.y + (double)out.z * rr.z : 0.0;
         for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-        __shared__ double sw[kApplyThreads / 64];
+        __shared__ double sw[WPB];
         if (lane == 0) sw[threadIdx.x >> 6] = a;
         __syncthreads();
         if (threadIdx.x == 0) {
             double t = 0.0;
-            for (int w = 0; w < kApplyThreads / 64; ++w) t += sw[w];
+            for (int w = 0; w < WPB; ++w) t += sw[w];
             rzPart[blockIdx.x] = t;
         }
     }
 }
 
 
-template <int NPROL, int VAR, bool RZ>
-__global__ __launch_bounds__(kApplyThreads) void k_solve_fine(const float4* __restrict__ inv, int blk0, int nFineBlk,
-                                                             int nV, const float4* __restrict__ r,
-                                                             const int4* __restrict__ vmap,
-                                                             const float4* __restrict__ zc, int begin1,
-                                                             float4* __restrict__ z, const int* __restrict__ done,
-                                                             double* __restrict__ rzPart) {
+// WPB blocks (waves) per workgroup: 2 by default (MAS_FINE_VARIANT=6) -- two-
+// wave workgroups, XCD-chunked, measured interleaved against four-wave ones,
+// bitwise equal (profiles/round4/ab/fine_wpb/): 1M + contacts 113.0 -> 112.0
+// us per apply, 256k 32.03 -> 31.78, 4M tet 453.6 -> 451.3 (one-wave
+// workgroups: better at 1M, worse at 256k and 4M).
+template <int NPROL, int VAR, bool RZ, int WPB = kApplyThreads / 64>
+__global__ __launch_bounds__(64 * WPB) void k_solve_fine(const float4* __restrict__ inv, int blk0, int nFineBlk,
+                                                        int nV, const float4* __restrict__ r,
+                                                        const int4* __restrict__ vmap,
+                                                        const float4* __restrict__ zc, int begin1,
+                                                        float4* __restrict__ z, const int* __restrict__ done,
+                                                        double* __restrict__ rzPart) {
     if (RZ && *done) return;
-    solve_fine_body<NPROL, VAR, RZ>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, rzPart);
-}
-
-// A/B (MAS_FINE_VARIANT=6): the chunked form in two-wave workgroups (twice
-// as many, XCD-chunked: a finer last round at 256k's 2.7 rounds of waves).
-template <int NPROL>
-__global__ __launch_bounds__(128) void k_solve_fine2(const float4* __restrict__ inv, int blk0, int nFineBlk, int nV,
-                                                    const float4* __restrict__ r, const int4* __restrict__ vmap,
-                                                    const float4* __restrict__ zc, int begin1, float4* __restrict__ z) {
-    solve_fine_body<NPROL, 4, false, 2>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, nullptr);
+    solve_fine_body<NPROL, VAR, RZ, WPB>(inv, blk0, nFineBlk, nV, r, vmap, zc, begin1, z, rzPart);
 }
 
 // A/B (MAS_FINE_VARIANT=7): the chunked form in one-wave workgroups.
@@ -281,11 +277,14 @@ template <int NPROL>
 static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int blk0, int blkEnd, int nV,
                           const float4* r, const int4* vmap, const float4* zc, int begin1, float4* z,
                           const int* done, double* rzPart) {
-    if (rzPart) {  // the PCG driver's applies
-        if (var == 0)
+    if (rzPart) {  // the PCG driver's applies (fine_grid(h) workgroups: one r.z partial each)
+        if (var == 6)
+            k_solve_fine<NPROL, 4, true, 2><<<cdiv(blkEnd - blk0, 2), 128, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
+                                                                                 begin1, z, done, rzPart);
+        else if (var == 0)
             k_solve_fine<NPROL, 0, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                        done, rzPart);
-        else if (var == 4)
+        else if (var >= 4)  // 4, 5, 7: four-wave workgroups
             k_solve_fine<NPROL, 4, true><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                        done, rzPart);
         else
@@ -297,7 +296,8 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
         k_solve_fine<NPROL, 4, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                     nullptr, nullptr);
     } else if (var == 6) {
-        k_solve_fine2<NPROL><<<cdiv(blkEnd - blk0, 2), 128, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
+        k_solve_fine<NPROL, 4, false, 2><<<cdiv(blkEnd - blk0, 2), 128, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
+                                                                               begin1, z, nullptr, nullptr);
     } else if (var == 7) {
         k_solve_fine1c<NPROL><<<blkEnd - blk0, 64, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
     } else if (var == 0) {
@@ -328,7 +328,7 @@ void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* 
     }
 }
 
-int fine_grid(const mas_context* h) { return cdiv(h->nFineBlk, kApplyThreads / 64); }
+int fine_grid(const mas_context* h) { return cdiv(h->nFineBlk, h->fineVariant == 6 ? 2 : kApplyThreads / 64); }
 
 // coarse levels lFirst..L-1: level 1 from the vertices (k_coarse_l1), level
 // 2 from R1 (k_coarse_up), levels >= 3 in one k_coarse_deep launch (R folded

@@ -191,11 +191,12 @@ struct mas_context {
     int coarseOcc = -1;
     int coarseWide = 0;     // k_solve123 in 512-thread workgroups (env MAS_COARSE_WIDE)
     int coarseNarrow = -1;  // single-wave coarse workgroups: -1 = at L = 3, 0 = never, 1 = always (env MAS_COARSE_NARROW)
-    // fine kernel (env MAS_FINE_VARIANT, k_apply.hip): 4 = nontemporal inverse
-    // loads, 4-wave workgroups dealt to the XCDs in contiguous chunks; 1 = the
-    // same without the chunking (A/B); 3 = 1 in one-wave workgroups (A/B);
-    // 0 = default-policy loads (A/B)
-    int fineVariant = 4;
+    // fine kernel (env MAS_FINE_VARIANT, k_apply.hip): 6 = nontemporal inverse
+    // loads, 2-wave workgroups dealt to the XCDs in contiguous chunks; 4 = the
+    // same in 4-wave workgroups, 7 in one-wave ones (A/B); 1 = 4 without the
+    // chunking (A/B); 3 = 1 in one-wave workgroups (A/B); 0 = default-policy
+    // loads (A/B)
+    int fineVariant = 6;
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     int nStencilEF = 0;  // of nStencil, the EF stencils (at most 5 vertices; EE / VF have 4)
     int nBlkPrev = 0;  // nBlk of the previous Prepare, read by the early path's thread (run_levels may change nBlk meanwhile)
