@@ -103,7 +103,6 @@ struct Coarse1Args {
     int nb1;
     int pollDelay;        // fold / solve waves: s_sleep(64) rounds before the first poll (A/B)
     int chunk;            // bank waves XCD-chunked (as k_apply.hip xcd_chunked): Morton-adjacent banks share an L2
-    int prefetch;         // bank waves issue their level-1 record behind the r gathers (A/B)
     const int* done;      // PCG: exit at once when set
     int pollLimit;        // polls before a wait gives up (kPollLimit; < 0: give up at once, a test knob)
     int* timeouts;        // waits that gave up: this apply's z is incomplete (mas_stats.wait_timeouts)
@@ -135,9 +134,6 @@ __device__ __forceinline__ void bank_wave(const Coarse1Args& a, int B, C1Shared&
     float4 val[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) val[q] = src[q] >= 0 ? a.r[src[q]] : make_float4(0.f, 0.f, 0.f, 0.f);
-    // the Z1 record: behind the gathers (prefetch) or after the publications
-    float g[kRecord], tl[3];
-    if (a.prefetch) load_record<true>(a.inv, a.begin1 / 32 + B, lane, g, tl);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         sh.bank.svs[0][2 * q + (lane >> 5)][j] = val[q].x;
@@ -193,7 +189,8 @@ __device__ __forceinline__ void bank_wave(const Coarse1Args& a, int B, C1Shared&
     C1_STAMP(1, B, 2);
     // Z1 of the bank's block from the R1 in registers (inverse loaded after the
     // publications, so the restriction's gathers do not queue behind it)
-    if (!a.prefetch) load_record<true>(a.inv, a.begin1 / 32 + B, lane, g, tl);
+    float g[kRecord], tl[3];
+    load_record<true>(a.inv, a.begin1 / 32 + B, lane, g, tl);
     const float3 out = block_solve(g, tl, make_float3(__shfl(ax, j), __shfl(ay, j), __shfl(az, j)), lane);
     if (lane < 32) a.zc[c] = make_float4(out.x, out.y, out.z, 0.f);
     C1_STAMP(1, B, 3);
@@ -424,7 +421,6 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.epoch = h->coarse1Epoch;
     a.pollDelay = h->c1PollDelay;
     a.chunk = h->c1Chunk;
-    a.prefetch = h->c1Prefetch;
     a.done = h->applyDone;
     a.pollLimit = h->c1PollLimit;
     a.members = h->groupedR3 && deep ? P<int2>(h->members) : nullptr;

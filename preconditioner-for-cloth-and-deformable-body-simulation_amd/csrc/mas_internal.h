@@ -297,7 +297,6 @@ struct mas_context {
     // pre-fine 14.65 -> 13.82 us at 1M + contacts, 47.5 -> 42.5 us at 4M tet
     // (profiles/round4/ab/c1chunk_*.json)
     int c1Chunk = 1;
-    int c1Prefetch = 0;   // A/B (env MAS_C1_PREFETCH): bank waves load their level-1 record behind the r gathers
     // k_coarse1's bounded waits never hang the device: a wait gives up after
     // this many polls and is counted (env MAS_C1_POLL_LIMIT; < 0 forces it: tests)
     int c1PollLimit = 1 << 16;
