@@ -10,11 +10,17 @@ star's 1-GPU roofline target is quoted on.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): the same 1M
-problem is sharded by Morton range (strong scaling): rank g solves its own
-level-0 blocks, one RCCL allgather of the level-1 residual segments per apply,
-coarse levels >= 2 redundant.  value = applies of the whole
-problem per second (max time over ranks).  Rank 0 prints ONE JSON line.
+N > 1 (one rank per GPU): the same 1M problem is sharded by Morton range
+(strong scaling): rank g solves its own level-0 blocks, one RCCL allgather of
+the level-1 residual segments per apply, coarse levels >= 2 redundant
+(DESIGN.md §7).  value = applies of the whole problem per second (max time
+over ranks).  Rank 0 prints ONE JSON line.  Run under torch.distributed.run
+(WORLD_SIZE set: --gpus must equal it), or plainly as `python bench.py --gpus
+N`: then this process starts `python -m torch.distributed.run --nproc-per-node
+N bench.py ...` as a child before anything touches the GPU, forwards rank 0's
+JSON line and exits with the child's status.  With the nccl backend every rank
+needs its own device (LOCAL_RANK < device count, else a loud failure); the gloo
+backend may put several ranks on one GPU (a one-GPU rehearsal of N > 1).
 
 roofline: the dominant kernel is the fused fine-level kernel (gather r through
 the Morton map, 32-node block solves, prolongation, scatter z).  Its
@@ -181,6 +187,78 @@ def cpu_baseline(mesh, cfg, contacts, r_np, steps):
 PREP_KEYS = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms", "prepare_fine_ms")
 
 
+class LaunchError(SystemExit):
+    """A rank/device layout that cannot run: exit status 2 with the reason."""
+
+    def __init__(self, msg):
+        log(f"bench.py: {msg}")
+        super().__init__(2)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(argv, gpus, env):
+    """The torch.distributed.run command a plain `bench.py --gpus N` (N > 1)
+    starts as its child, or None when this process is a rank already
+    (WORLD_SIZE set by a launcher) or N == 1."""
+    if "WORLD_SIZE" in env or gpus <= 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+            os.path.abspath(__file__), *argv]
+
+
+def run_launcher(cmd):
+    """Run the ranks as ONE child process tree (never an exec: nothing in this
+    process has touched the GPU, and nothing will); rank 0's JSON line goes to
+    stdout, every other line of the children's stdout to stderr."""
+    import subprocess
+    log("bench.py: launching " + " ".join(cmd[1:]))
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            print(s, flush=True)
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    return p.wait()
+
+
+def check_rank_layout(gpus, world, local, ndev, backend):
+    """Under a launcher: --gpus must equal WORLD_SIZE; with nccl (RCCL) every
+    rank needs a device of its own.  Returns the device index for this rank."""
+    if gpus != world:
+        raise LaunchError(f"--gpus {gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                          f"(torch.distributed.run --nproc-per-node {gpus})")
+    if ndev <= 0:
+        raise LaunchError("no GPU visible (torch.cuda.device_count() == 0)")
+    if local < ndev:
+        return local
+    if backend == "nccl":
+        raise LaunchError(f"LOCAL_RANK {local} needs GPU {local}, but only {ndev} GPU(s) are visible: "
+                          f"the nccl (RCCL) backend runs one rank per GPU; use --dist-backend gloo to "
+                          f"rehearse {world} ranks on fewer GPUs")
+    return local % ndev  # gloo rehearsal: ranks share the visible GPUs
+
+
+def launch_check(args, rank, world, local):
+    """--launch-check: each rank reports its layout and exits before any GPU
+    work (the CPU test of the launcher)."""
+    import torch
+    out = {"rank": rank, "world": world, "local_rank": local, "gpus": args.gpus,
+           "device_count": torch.cuda.device_count()}
+    if rank == 0:
+        print(json.dumps({"metric": "launch-check", **out}), flush=True)
+    else:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -200,20 +278,39 @@ def main():
                          "call per apply) or an allgather hook through torch.distributed")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo only to exercise N>1 on one GPU")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher test: every rank reports its layout and exits before any GPU work")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise LaunchError(f"--gpus {args.gpus}: need at least 1")
+
+    # N > 1 without a launcher: start the ranks as a child process before
+    # anything here loads HIP (no torch.cuda call, no library load).
+    cmd = launcher_command(sys.argv[1:], args.gpus, os.environ)
+    if cmd is not None:
+        if args.dist_backend == "nccl" and not args.launch_check:
+            import torch  # device_count() does not initialise the GPU
+            ndev = torch.cuda.device_count()
+            if ndev < args.gpus:
+                raise LaunchError(f"--gpus {args.gpus} with the nccl (RCCL) backend needs {args.gpus} GPUs, "
+                                  f"{ndev} visible; use --dist-backend gloo to rehearse {args.gpus} ranks on "
+                                  f"fewer GPUs")
+        sys.exit(run_launcher(cmd))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        check_rank_layout(args.gpus, world, local, max(world, 1), args.dist_backend)
+        launch_check(args, rank, world, local)
+        return
 
     import numpy as np
     import torch
     import mas_amd
     from mas_amd import meshgen
 
-    ndev = torch.cuda.device_count()
-    if ndev and local >= ndev:  # rehearsal of N > 1 on a one-GPU box (gloo backend)
-        local = local % ndev
+    local = check_rank_layout(args.gpus, world, local, torch.cuda.device_count(), args.dist_backend)
     torch.cuda.set_device(local)
     dist = None
     sharded_path = world > 1 or args.sharded
@@ -351,8 +448,16 @@ def main():
         pt = torch.tensor([st0[k] for k in PREP_KEYS], device="cuda", dtype=torch.float64)
         dist.all_reduce(pt, op=dist.ReduceOp.MAX)
         st0 = dict(st0, **dict(zip(PREP_KEYS, pt.tolist())))
+        props = torch.cuda.get_device_properties(local)
+        me = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "handle_device": local,
+              "current_device": torch.cuda.current_device(), "z_device": z.device.index,
+              "gpu_uuid": str(getattr(props, "uuid", "")) or None}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
         shard_check = {"own_slices_bitwise_equal_unsharded": bool(ok.item() == 1.0),
-                       "form": "overlapped (fine during allgather)" if sharded.overlap else "serial"}
+                       "form": "overlapped (fine during allgather)" if sharded.overlap else "serial",
+                       "backend": args.dist_backend, "ranks": ranks,
+                       "distinct_gpus": len({r["gpu_uuid"] or r["handle_device"] for r in ranks})}
 
     fine_bytes, apply_bytes = algorithmic_bytes(info)
     if plan is not None:  # the rank's own level-0 blocks and vertices
@@ -442,6 +547,9 @@ def main():
         "factor_formation": ("level-0 inverses Inv = L^-T D^-1 L^-1 on the matrix cores (v_mfma_f32_32x32x2_f32)"
                              if st0.get("factor_formation") == 1 else
                              "level-0 inverses in the reference's operation order on the vector ALUs"),
+        # the handle's mas_config switches (include/mas_capi.h): 0 = the tolerance-mode defaults (z within
+        # 1e-5 of the reference arithmetic), 1 = the reference's own operation order, bitwise
+        "mas_config": {"reference_formation": 0, "reference_restriction": 0},
         "allocate_ms": round(st0["allocate_ms"], 3),
         "host_setup_s": round(setup_s, 2),
         "wall_s_timed": round(wall, 4),

@@ -47,7 +47,12 @@ extern "C" {
 /* 3: MAS_ERR_NOT_SPD; mas_config.reference_restriction; mas_stats' reserved
  *    tail now carries hier_dirty_level, hier_rebuilt, prepare_fine_start_ms,
  *    nonspd_blocks, wait_timeouts (same sizes). */
-#define MAS_ABI_VERSION 3
+/* 4: mas_config.strict_spd (from the reserved tail, same size): a non-SPD
+ *    pivot fails Prepare only when set; by default Prepare returns MAS_OK,
+ *    counts the blocks in mas_stats.nonspd_blocks and leaves a warning in
+ *    mas_last_error, as the reference keeps going.  mas_apply_device reports
+ *    an earlier apply's coarse give-up (MAS_ERR_HIP) before queueing. */
+#define MAS_ABI_VERSION 4
 
 typedef enum {
     MAS_OK = 0,
@@ -59,10 +64,11 @@ typedef enum {
     MAS_ERR_NOMEM = -6,    /* device allocation failed                           */
     MAS_ERR_NO_DEVICE = -7, /* no HIP device / kernels not loadable               */
     MAS_ERR_COMM = -8,      /* the allgather hook / RCCL failed (see mas_last_error) */
-    MAS_ERR_NOT_SPD = -9    /* Prepare: a block's LDL^T met a zero, negative or non-finite pivot
-                               (mas_stats.nonspd_blocks; mas_last_error names the first block).  The
-                               reference divides by such pivots unchecked (.cpp:1406,1431); here the
-                               handle stays prepared with the same inverses, but the call fails */
+    MAS_ERR_NOT_SPD = -9    /* Prepare with mas_config.strict_spd = 1: a block's LDL^T met a zero,
+                               negative or non-finite pivot (mas_stats.nonspd_blocks; mas_last_error
+                               names the first block).  The reference divides by such pivots unchecked
+                               (.cpp:1406,1431); here the handle stays prepared with the same inverses,
+                               but the call fails.  Without strict_spd the call returns MAS_OK */
 } mas_status;
 
 typedef struct mas_context* mas_handle;
@@ -87,7 +93,11 @@ typedef struct {
                                   (BuildResidualHierarchy .cpp:1581-1590: every R1 folded into R3 in
                                   level-1 id order, a 1 024-add chain at 1M): the whole residual
                                   hierarchy bitwise the reference arithmetic, ~6 us more per apply */
-    int reserved[9];
+    int strict_spd;    /* ABI 4.  0 = as the reference, Prepare keeps going over a zero / negative /
+                          non-finite pivot: MAS_OK, mas_stats.nonspd_blocks > 0 and a warning in
+                          mas_last_error (an SPD but ill-conditioned Hessian can meet one in fp32);
+                          1 = such a Prepare fails with MAS_ERR_NOT_SPD */
+    int reserved[8];
 } mas_config;
 
 typedef struct {
@@ -134,7 +144,10 @@ typedef struct {
     double prepare_fine_start_ms; /* the fused level-0 kernel's start, after the Prepare's start */
     int64_t nonspd_blocks;     /* the last Prepare: blocks whose factor met a zero / negative / non-finite pivot */
     int64_t wait_timeouts;     /* since mas_create: bounded device waits of the one-launch coarse form that
-                                  gave up (the apply's z is then incomplete); mas_apply fails on one */
+                                  gave up (that apply's z is then incomplete), as of the latest such apply
+                                  (waits for it, not for the device).  The apply that gave up is named by
+                                  MAS_ERR_HIP from mas_apply / the PCG solve itself, or for mas_apply_device
+                                  from the next mas_apply* / PCG call on the handle */
     int64_t reserved[3];       /* zero; room for later fields without a size change */
 } mas_stats;
 

@@ -106,8 +106,18 @@ struct Coarse1Args {
     const int* done;      // PCG: exit at once when set
     int pollLimit;        // polls before a wait gives up (kPollLimit; < 0: give up at once, a test knob)
     int* timeouts;        // waits that gave up: this apply's z is incomplete (mas_stats.wait_timeouts)
+    int* giveupHost;      // pinned host word: the epoch of an apply whose wait gave up (the next call reports it)
     const int2* members;  // grouped level 3: per coarse node (child bank, child mask); null: the reference's fold
 };
+
+// A bounded wait gave up: count it on the device (mas_stats.wait_timeouts) and
+// name this apply in the handle's pinned host word with a system-scope vector
+// store, which the next host call reads without synchronising (mas_capi.hip
+// pending_giveup).
+__device__ __forceinline__ void gave_up(const Coarse1Args& a) {
+    atomicAdd(a.timeouts, 1);
+    __hip_atomic_store(a.giveupHost, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 union C1Shared {
     struct {
@@ -230,7 +240,7 @@ __device__ __forceinline__ void fold_wave(const Coarse1Args& a, int T, C1Shared&
         const int p = min(bad, n);
         if (p == 0) {
             if (a.pollLimit < 0 || ++idle > a.pollLimit) {  // never hang: the fold stays incomplete, and says so
-                if (lane == 0) atomicAdd(a.timeouts, 1);
+                if (lane == 0) gave_up(a);
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -286,7 +296,7 @@ __device__ __forceinline__ void fold_wave_grouped(const Coarse1Args& a, int T) {
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
     }
-    if (!__all(ok) && lane == 0) atomicAdd(a.timeouts, 1);  // R3 from stale R2: counted
+    if (!__all(ok) && lane == 0) gave_up(a);  // R3 from stale R2: counted
     C1_STAMP(0, T, 1);
     const float x = child ? tag_val(v[0]) : 0.f, y = child ? tag_val(v[1]) : 0.f, z = child ? tag_val(v[2]) : 0.f;
     float ax = 0.f, ay = 0.f, az = 0.f;
@@ -326,7 +336,7 @@ __device__ __forceinline__ void solve_wave(const Coarse1Args& a, int blk, int lv
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
     }
-    if (!__all(ok) && lane == 0) atomicAdd(a.timeouts, 1);  // solved from stale R: counted
+    if (!__all(ok) && lane == 0) gave_up(a);  // solved from stale R: counted
     C1_STAMP(2, slot, 1);
     // half 1 takes node n's residual from lane n (padding nodes: +0)
     const float rx = __shfl(tag_val(v[0]), n), ry = __shfl(tag_val(v[1]), n), rz = __shfl(tag_val(v[2]), n);
@@ -425,8 +435,13 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.pollLimit = h->c1PollLimit;
     a.members = h->groupedR3 && deep ? P<int2>(h->members) : nullptr;
     a.timeouts = P<int>(h->devStatus) + 2;
+    a.giveupHost = h->c1Host;
     h->c1Launched = true;
     k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3, 64, 0, s>>>(a);
+    // mas_get_stats waits for this event (the latest one-launch apply, on
+    // whatever stream it ran), not for the whole device; run_apply never
+    // launches this form on a capturing stream
+    hipEventRecord(h->evC1, s);
 }
 
 }  // namespace mas

@@ -730,6 +730,7 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
             const float4* d_b, int maxIters, float tol, int precondition, mas_pcg_result* res, hipStream_t s) {
     const int nV = h->nV;
     int rc;
+    if (precondition && (rc = pending_giveup(h))) return rc;  // an earlier apply's incomplete z, first
     if ((rc = ensure(h, h->pcgVec, (size_t)nV * (16 * 4 + sizeof(X64)))) ||
         (rc = ensure(h, h->pcgPartial, (size_t)kPcgBlocks * kParts * sizeof(double))) ||
         (rc = ensure(h, h->pcgState, sizeof(PcgState))))
@@ -769,7 +770,7 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
         res->replacements = host.replacements;
     }
     if ((rc = hip_check(h, hipGetLastError(), "pcg kernels"))) return rc;
-    return take_wait_timeouts(h, s);  // a preconditioner apply whose coarse hand-off gave up fails the solve
+    return pending_giveup(h);  // a preconditioner apply whose coarse hand-off gave up fails the solve
 }
 
 }  // namespace mas

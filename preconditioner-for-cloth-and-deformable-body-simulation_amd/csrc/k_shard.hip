@@ -289,6 +289,7 @@ int mas_shard_setup(mas_handle h, int rank, int world, mas_shard* out) {
 int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r4, float* d_seg4, void* stream) {
     if (!h || !d_r4 || !d_seg4) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    hipSetDevice(h->device);  // ensure() allocates on the current device (shard_coarse's tables)
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
     if (rc) return rc;
@@ -354,6 +355,7 @@ int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gat
                            float* d_z4, void* stream) {
     if (!h || !d_gathered4 || !d_r4 || !d_z4) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    hipSetDevice(h->device);  // ensure() allocates on the current device (shard_coarse's tables)
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
     if (rc) return rc;
@@ -378,6 +380,7 @@ int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gat
 int mas_apply_shard_fine(mas_handle h, int rank, int world, const float* d_r4, float* d_z4, void* stream) {
     if (!h || !d_r4 || !d_z4) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    hipSetDevice(h->device);  // ensure() allocates on the current device (shard_coarse's tables)
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
     if (rc) return rc;
@@ -399,6 +402,7 @@ int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_g
                              void* stream) {
     if (!h || !d_gathered4 || !d_z4) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    hipSetDevice(h->device);  // ensure() allocates on the current device (shard_coarse's tables)
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
     if (rc) return rc;

@@ -120,20 +120,12 @@ int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> s
     return rc ? rc : read_back_wait(h, s, seq, out, (int)src.size());
 }
 
-int take_wait_timeouts(mas_context* h, hipStream_t s) {
-    if (!h->c1Launched || !h->devStatus.p) return MAS_OK;
-    h->c1Launched = false;
-    int n = 0;
-    int* w = P<int>(h->devStatus) + 2;
-    int rc;
-    if ((rc = hip_check(h, hipMemcpyAsync(&n, w, 4, hipMemcpyDeviceToHost, s), "read status")) ||
-        (rc = hip_check(h, hipStreamSynchronize(s), "read status")))
-        return rc;
-    if (n == 0) return MAS_OK;
-    h->waitTimeouts += n;
-    if ((rc = hip_check(h, hipMemsetAsync(w, 0, 4, s), "clear status"))) return rc;
-    return fail(h, MAS_ERR_HIP, std::to_string(n) + " bounded hand-off wait(s) of the one-launch coarse form gave "
-                                "up (k_coarse1): the coarse part of z is incomplete");
+int pending_giveup(mas_context* h) {
+    if (!h->c1Host) return MAS_OK;
+    const int epoch = __atomic_exchange_n(h->c1Host, 0, __ATOMIC_ACQ_REL);
+    if (epoch == 0) return MAS_OK;
+    return fail(h, MAS_ERR_HIP, "apply #" + std::to_string((unsigned)epoch) + " (k_coarse1): a bounded hand-off wait "
+                "gave up, so that apply's coarse part of z is incomplete (mas_stats.wait_timeouts counts the waits)");
 }
 
 static void release(Buffer& b) {
@@ -183,6 +175,16 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
         return MAS_ERR_HIP;
     }
     for (auto& e : h->ev) hipEventCreate(&e);
+    {
+        void* p = nullptr;
+        if (hipEventCreateWithFlags(&h->evC1, hipEventDisableTiming) != hipSuccess ||
+            hipHostMalloc(&p, 64, hipHostMallocCoherent) != hipSuccess) {
+            mas_destroy(h);
+            return MAS_ERR_HIP;
+        }
+        h->c1Host = static_cast<int*>(p);
+        std::memset(p, 0, 64);
+    }
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_OCC")) h->coarseOcc = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_NARROW")) h->coarseNarrow = std::atoi(v);
@@ -249,6 +251,8 @@ int mas_destroy(mas_handle h) {
     if (h->evShardDone) hipEventDestroy(h->evShardDone);
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->rbHost) hipHostFree(h->rbHost);
+    if (h->evC1) hipEventDestroy(h->evC1);
+    if (h->c1Host) hipHostFree(h->c1Host);
     delete h;
     return MAS_OK;
 }
@@ -317,6 +321,9 @@ int mas_apply_device(mas_handle h, float* d_z4, const float* d_r4, void* stream)
     if ((reinterpret_cast<uintptr_t>(d_z4) | reinterpret_cast<uintptr_t>(d_r4)) & 15)
         return fail(h, MAS_ERR_ARG, "mas_apply_device: vectors must be 16-byte aligned");
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    // an earlier apply (device or host) whose coarse hand-off gave up is
+    // reported here, before this one is queued: its z was incomplete
+    MAS_TRY(pending_giveup(h));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     return run_apply(h, reinterpret_cast<float4*>(d_z4), reinterpret_cast<const float4*>(d_r4), s);
 }
@@ -367,6 +374,7 @@ int mas_apply(mas_handle h, float* z4, const float* r4) {
     if (!h) return MAS_ERR_ARG;
     if (!z4 || !r4) return fail(h, MAS_ERR_ARG, "mas_apply: null vector");
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    MAS_TRY(pending_giveup(h));  // an earlier device apply's incomplete z, first
     hipSetDevice(h->device);
     const size_t bytes = (size_t)h->nV * 16;
     MAS_TRY(ensure(h, h->rStage, bytes));
@@ -375,7 +383,7 @@ int mas_apply(mas_handle h, float* z4, const float* r4) {
     MAS_TRY(run_apply(h, P<float4>(h->zStage), P<float4>(h->rStage), h->stream));
     MAS_TRY(hip_check(h, hipMemcpyAsync(z4, h->zStage.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H z"));
     MAS_TRY(hip_check(h, hipStreamSynchronize(h->stream), "apply sync"));
-    return take_wait_timeouts(h, h->stream);  // a synchronous apply reports an incomplete z
+    return pending_giveup(h);  // a synchronous apply reports its own incomplete z
 }
 
 int mas_set_profiling(mas_handle h, int enable) {
@@ -436,14 +444,18 @@ int mas_get_stats(mas_handle h, mas_stats* out) {
         h->stats.post_fine_ms_avg = sc / n;
     }
     h->stats.apply_mode = coarse_mode(h);
-    if (h->c1Launched) {  // the counter of waits that gave up, after every apply queued so far
+    if (h->c1Launched) {
+        // the waits that gave up, counted on the device since mas_create, as of
+        // the latest one-launch apply (on whatever stream it ran): waits for that
+        // apply's event and the handle's stream only, never the whole device
         hipSetDevice(h->device);
-        hipDeviceSynchronize();
-        const std::string keep = h->err;
-        take_wait_timeouts(h, h->stream);  // counted here; the error itself is mas_apply's to return
-        h->err = keep;
+        int n = 0;
+        if (hipEventSynchronize(h->evC1) != hipSuccess ||
+            hipMemcpyAsync(&n, P<int>(h->devStatus) + 2, 4, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+            return fail(h, MAS_ERR_HIP, "mas_get_stats: reading the wait counter");
+        h->stats.wait_timeouts = n;
     }
-    h->stats.wait_timeouts = h->waitTimeouts;
     *out = h->stats;
     return MAS_OK;
 }

@@ -300,11 +300,14 @@ struct mas_context {
     // k_coarse1's bounded waits never hang the device: a wait gives up after
     // this many polls and is counted (env MAS_C1_POLL_LIMIT; < 0 forces it: tests)
     int c1PollLimit = 1 << 16;
-    bool c1Launched = false;    // k_coarse1 ran since devStatus[2] was last read
+    bool c1Launched = false;    // k_coarse1 ran since the handle was created (evC1 has been recorded)
+    hipEvent_t evC1 = nullptr;  // after the latest k_coarse1 launch (mas_get_stats waits for it)
+    // pinned host-coherent word: the epoch of the latest apply whose k_coarse1
+    // wait gave up, 0 when none since the last report (pending_giveup)
+    int* c1Host = nullptr;
     // device status words: [0] blocks with a bad pivot (this Prepare), [1] the
-    // lowest such block, [2] coarse hand-off waits that gave up (since read)
+    // lowest such block, [2] coarse hand-off waits that gave up (since mas_create)
     mas::Buffer devStatus;
-    long long waitTimeouts = 0;  // [2] accumulated on the host
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
     mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
     mas::Buffer pcgRzPart;                               // PCG: r.z partials of the fine apply kernel
@@ -454,9 +457,10 @@ int fine_grid(const mas_context* h);  // workgroups of one fine launch over ever
 int compute_l1_first(mas_context* h, hipStream_t s);
 // up to 8 device ints -> out, through pinned memory (mas_capi.hip)
 int read_back(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* out);
-// devStatus[2] (coarse hand-off waits that gave up) -> h->waitTimeouts, after
-// the work that may have set it is complete; MAS_ERR_HIP when new ones came
-int take_wait_timeouts(mas_context* h, hipStream_t s);
+// MAS_ERR_HIP when an apply's k_coarse1 wait gave up since the last report
+// (reads and clears the pinned word c1Host; no synchronisation): an apply
+// that completed with an incomplete z is reported by the next call
+int pending_giveup(mas_context* h);
 // the same split in two: enqueue the copy (its sequence number in *seq), and
 // later wait for it (or a newer post) to land
 int read_back_post(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* seq);

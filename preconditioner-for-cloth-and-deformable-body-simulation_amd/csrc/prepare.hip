@@ -18,6 +18,7 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
                 hipStream_t s) {
     int rc;
     h->prepared = false;
+    h->err.clear();  // after a successful Prepare: empty, or the non-SPD warning
     hipEventRecord(h->ev[2], s);
     // pivot checks of this Prepare's factors: [0] count, [1] lowest block (k_factor.hip check_pivots)
     int* status = P<int>(h->devStatus);
@@ -49,9 +50,15 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     // could allocate it twice and leave them with different pointers
     if (early && (rc = early_buffers(h))) return rc;
     // the worker's job never outlives this call, whatever path returns
+    // (on an error return of this thread: joined without reporting, so
+    // mas_last_error keeps this thread's message, not the worker's)
     struct JoinEarly {
         mas_context* h;
-        ~JoinEarly() { finish_early(h); }
+        ~JoinEarly() {
+            if (!h->earlyPending) return;
+            h->prepWorker->wait();
+            h->earlyPending = false;
+        }
     } joinEarly{h};
     if (early && h->earlyThread) {
         // a second host thread queues prepStream's work while this one queues
@@ -134,9 +141,13 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
         int level = 0;
         for (int l = 1; l < h->L; ++l)
             if (32 * bad[1] >= h->levelSize[2 * l + 1]) level = l;
-        return fail(h, MAS_ERR_NOT_SPD, std::to_string(bad[0]) + " block(s) met a zero, negative or non-finite "
-                    "pivot in LDL^T (first: block " + std::to_string(bad[1]) + ", level " + std::to_string(level) +
-                    "): the Hessian is not SPD there; the reference divides by it unchecked (.cpp:1406,1431)");
+        const std::string msg = std::to_string(bad[0]) + " block(s) met a zero, negative or non-finite pivot in "
+                                "LDL^T (first: block " + std::to_string(bad[1]) + ", level " + std::to_string(level) +
+                                "): the Hessian is not SPD there; the reference divides by it unchecked "
+                                "(.cpp:1406,1431)";
+        // strict_spd: fail; else keep going as the reference does, with a warning
+        if (h->cfg.strict_spd) return fail(h, MAS_ERR_NOT_SPD, msg);
+        fail(h, MAS_OK, "warning: " + msg);
     }
     return MAS_OK;
 }

@@ -4,6 +4,8 @@
 // mapping and the memory layouts.
 #include "SeSchwarzPreconditioner.h"
 
+#include <cstdio>
+#include <cstring>
 #include <string>
 
 int CPU_THREAD_NUM = 1;  // SeOmp.cpp:29-33; the GPU path has no CPU threads
@@ -47,6 +49,10 @@ void SeSchwarzPreconditioner::PreparePreconditioner(const SeMatrix3f* diagonal, 
     Check(mas_prepare(m_handle, diagonal->m_data, csrOffDiagonals->m_data, csrRanges, efSets, eeSets, vfSets,
                       efCounts, eeCounts, vfCounts),
           "PreparePreconditioner");
+    // a non-SPD pivot (mas_config.strict_spd = 0): keep going as the reference
+    // does (its method is void), but say so
+    const char* w = mas_last_error(m_handle);
+    if (w && std::strncmp(w, "warning:", 8) == 0) std::fprintf(stderr, "SeSchwarzPreconditioner: %s\n", w);
 }
 
 void SeSchwarzPreconditioner::Preconditioning(SeVec3fSimd* z, const SeVec3fSimd* residual, int /*dim*/) {

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
 
 import numpy as np
 
@@ -49,7 +50,7 @@ class mas_config(ctypes.Structure):
     _fields_ = [("max_levels", ctypes.c_int), ("resort_period", ctypes.c_int), ("fix_vf_bary", ctypes.c_int),
                 ("device", ctypes.c_int), ("keep_blocks", ctypes.c_int),
                 ("reference_formation", ctypes.c_int), ("reference_restriction", ctypes.c_int),
-                ("reserved", ctypes.c_int * 9)]
+                ("strict_spd", ctypes.c_int), ("reserved", ctypes.c_int * 8)]
 
 
 class mas_info(ctypes.Structure):
@@ -91,6 +92,10 @@ class mas_pcg_result(ctypes.Structure):
 
 class MasError(RuntimeError):
     pass
+
+
+class MasWarning(RuntimeWarning):
+    """Prepare met a non-SPD pivot and kept going (mas_config.strict_spd = 0)."""
 
 
 _lib = None
@@ -206,10 +211,11 @@ class SeSchwarzPreconditioner:
     """Reference-compatible surface (SE::SeSchwarzPreconditioner) on the GPU."""
 
     def __init__(self, max_levels: int = 0, resort_period: int = 0, fix_vf_bary: bool = False, device: int = -1,
-                 keep_blocks: bool = False, reference_formation: bool = False, reference_restriction: bool = False):
+                 keep_blocks: bool = False, reference_formation: bool = False, reference_restriction: bool = False,
+                 strict_spd: bool = False):
         self._L = lib()
         cfg = mas_config(max_levels, resort_period, int(fix_vf_bary), device, int(bool(keep_blocks)),
-                         int(bool(reference_formation)), int(bool(reference_restriction)))
+                         int(bool(reference_formation)), int(bool(reference_restriction)), int(bool(strict_spd)))
         h = ctypes.c_void_p()
         rc = self._L.mas_create(ctypes.byref(h), ctypes.byref(cfg))
         if rc != MAS_OK:
@@ -245,6 +251,13 @@ class SeSchwarzPreconditioner:
             msg = self._L.mas_last_error(self.h)
             raise MasError(f"{what} failed: {STATUS.get(rc, rc)}: {msg.decode() if msg else ''}")
 
+    def _warn_prepare(self, what):
+        """A Prepare that met a non-SPD pivot without strict_spd keeps going, as
+        the reference's void method does, with a MasWarning."""
+        msg = self._L.mas_last_error(self.h)
+        if msg and msg.startswith(b"warning:"):
+            warnings.warn(f"{what}: {msg.decode()}", MasWarning, stacklevel=3)
+
     # ---- the reference's three methods ----
     def AllocatePrecoditioner(self, numVerts, numEdges, numFaces):
         if self.m_neighbours is None:
@@ -277,6 +290,7 @@ class SeSchwarzPreconditioner:
         self._plans = {}
         self._check(self._L.mas_prepare(self.h, _ptr(d), _ptr(o), _ptr(r), _ptr(efSets), _ptr(eeSets), _ptr(vfSets),
                                         _ptr(efC), _ptr(eeC), _ptr(vfC)), "PreparePreconditioner")
+        self._warn_prepare("PreparePreconditioner")
 
     def PreparePreconditionerDevice(self, d_diag, d_off, d_ranges, efSets=None, eeSets=None, vfSets=None,
                                     efCounts=None, eeCounts=None, vfCounts=None, stream=None):
@@ -292,6 +306,7 @@ class SeSchwarzPreconditioner:
         self._check(self._L.mas_prepare_device(self.h, _ptr(d_diag), _ptr(d_off), _ptr(d_ranges), _ptr(efSets),
                                                _ptr(eeSets), _ptr(vfSets), _ptr(efC), _ptr(eeC), _ptr(vfC),
                                                _ptr(stream)), "PreparePreconditionerDevice")
+        self._warn_prepare("PreparePreconditionerDevice")
 
     def Preconditioning(self, z, residual, dim=None):
         self._need("Preconditioning")

@@ -150,3 +150,29 @@ def test_level3_handoff_across_xcds_4m_tet(grouped):
         s.synchronize()
         z.append(zd.cpu().numpy())
     np.testing.assert_array_equal(z[0], z[1])
+
+
+def test_reference_arithmetic_end_to_end():
+    """Both reference switches on (mas_config.reference_formation = 1 and
+    reference_restriction = 1): the level-0 inverses are bitwise the oracle's,
+    the whole residual hierarchy is, and z is within 1e-5 of the oracle's on
+    the default one-launch apply (1M + 100k contacts' shape at 256², L = 4)."""
+    import mas_amd
+    from mas_amd import meshgen
+    from oracle import Oracle
+    mesh = cloth(256)
+    contacts = meshgen.vf_contacts(mesh, 6000, seed=3)
+    P = mas_amd.from_mesh(mesh, max_levels=4, contacts=contacts, reference_formation=True,
+                          reference_restriction=True)
+    assert P.stats()["factor_formation"] == 0
+    o = Oracle(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0], 4, 8)
+    o.allocate(mesh)
+    o.prepare(mesh, vf=contacts[0], vfC=contacts[1])
+    nfine = (mesh.nV + 31) // 32
+    for blk in (0, nfine // 3, nfine - 1):
+        np.testing.assert_array_equal(P.block_inverse(blk), o.block_inverse(blk))
+    r = meshgen.residual(mesh.nV, 0x5EED)
+    _check(P, o, r, "reference arithmetic", grouped=False)
+    z_g, z_o = P.Preconditioning(None, r), o.apply(r)
+    err = float(np.linalg.norm((z_g - z_o)[:, :3]) / np.linalg.norm(z_o[:, :3]))
+    assert err <= 1e-5, err
