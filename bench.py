@@ -466,13 +466,7 @@ def main():
                       (plan["vert_end"] - plan["vert_begin"]) * (36 + 4 * (L4 - 1)))
     # the committed PMC figure is one whole-problem launch: a sharded rank's
     # launch moves only its own slice, so N > 1 lines carry no traffic figure
-    # the fused apply (apply_mode 4: coarse levels and level-0 blocks in one
-    # launch) is the whole apply in one kernel: its bytes are the apply's
-    fused = plan is None and st["apply_mode"] == 4 and info["num_levels"] >= 3
-    if fused:
-        fine_bytes = apply_bytes
-    kname = "k_apply_fused" if fused else "k_solve_fine"
-    traffic = pmc_traffic(kname) if plan is None else (None, None, {})
+    traffic = pmc_traffic("k_solve_fine") if plan is None else (None, None, {})
     fine_s = st["fine_ms_avg"] / 1e3
     achieved = fine_bytes / fine_s / 1e9 if fine_s > 0 else None
     value = args.steps / t_max          # applies of the whole problem per second
@@ -514,9 +508,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("k_apply_fused (every coarse level + level-0 block solves with the gather and the "
-                       "prolongation, one launch)" if fused else
-                       "k_solve_fine (fused gather + level-0 block solves + prolongation)"),
+            "kernel": "k_solve_fine (fused gather + level-0 block solves + prolongation)",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -539,8 +531,7 @@ def main():
             "coarse_launches": ("none (one level)" if info["num_levels"] <= 1 else
                                 "one per level" if info["num_levels"] == 2 else
                                 {0: "one per level", 2: "two (k_restrict12, k_solve123)",
-                                 3: "one (k_coarse1, tagged hand-offs)",
-                                 4: "none: inside k_apply_fused with the level-0 blocks"}[st["apply_mode"]]),
+                                 3: "one (k_coarse1, tagged hand-offs)"}[st["apply_mode"]]),
             "ms_per_step_with_kernel_events": round(elapsed_ev / args.steps * 1e3, 5),
         },
         "apply_algorithmic_GBps": round(apply_bytes / (t_max / args.steps) / 1e9, 1),

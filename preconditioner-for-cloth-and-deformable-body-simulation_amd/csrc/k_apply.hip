@@ -414,12 +414,9 @@ int coarse_mode(const mas_context* h) {
     return h->L == 3 || (h->L >= 4 && h->groupedR3) ? 3 : 2;
 }
 
-// the fused form (coarse levels + level-0 blocks in one launch, k_coarse1.hip
-// k_apply_fused) for this apply: mode 4, not for the PCG driver's applies
-// (their r.z comes from the fine kernel) nor on a capturing stream
-static bool use_fused(const mas_context* h, int mode, bool capturing) {
-    return mode == 4 && !capturing && !h->applyRzPart && h->L >= 3 && fused_supported(h);
-}
+// (A fused form -- the coarse levels and the level-0 blocks in one launch,
+// the fine waves reading tagged coarse Z -- was measured slower at every size
+// and removed: DESIGN.md section 4 "Fused apply".)
 
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     if (h->L >= 4 && !h->deepOff.p) return fail(h, MAS_ERR_STATE, "apply: deep-level lists not built");
@@ -434,17 +431,9 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     // would freeze: a capturing stream gets the two-launch form.
     const int mode = coarse_mode(h);
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    const bool capturing = h->L > 2 && mode >= 3 &&
+    const bool capturing = h->L > 2 && mode == 3 &&
                            (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone);
-    if (use_fused(h, mode, capturing)) {
-        if (ev) hipEventRecord(ev[1], s);
-        launch_apply_fused(h, d_r, d_z, s);
-        if (ev) hipEventRecord(ev[2], s);
-        if (ev) hipEventRecord(ev[3], s);
-        h->stats.apply_calls++;
-        return hip_check(h, hipGetLastError(), "apply kernels");
-    }
-    if (h->L > 2 && mode >= 3 && !capturing && coarse1_supported(h))
+    if (h->L > 2 && mode == 3 && !capturing && coarse1_supported(h))
         launch_coarse_one(h, d_r, s);
     else if (h->L > 2 && mode >= 2) launch_coarse_twopass(h, d_r, s);
     else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);

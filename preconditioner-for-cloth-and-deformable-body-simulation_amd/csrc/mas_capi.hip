@@ -198,8 +198,6 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_C1_POLL_DELAY")) h->c1PollDelay = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_CHUNK")) h->c1Chunk = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_POLL_LIMIT")) h->c1PollLimit = std::atoi(v);
-    if (const char* v = std::getenv("MAS_FUSE_EARLY")) h->fuseEarly = std::atoi(v);
-    if (const char* v = std::getenv("MAS_FUSE_HOLD")) h->fuseHold = std::atoi(v);
     if (const char* v = std::getenv("MAS_PREP_CU_RESERVE")) h->prepCuReserve = std::atoi(v);
     if (const char* v = std::getenv("MAS_FUSED_AFTER_LEVELS")) h->fusedAfterLevels = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_THREAD")) h->earlyThread = std::atoi(v);

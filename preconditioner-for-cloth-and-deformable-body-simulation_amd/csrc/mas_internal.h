@@ -290,13 +290,6 @@ struct mas_context {
     // lists, level-2 nodes, level-3 nodes), per level-1 node (parent, mask,
     // list slot); the apply epoch the tags carry (0 after Prepare)
     mas::Buffer c1Tags, l1info;
-    // fused apply (coarseMode 4, k_coarse1.hip): tagged coarse Z per coarse
-    // node, and the count of Z-producing coarse waves done
-    mas::Buffer tZ, fuseDef;
-    int fuseEarly = -1;      // fine workgroups beside the coarse chain (env MAS_FUSE_EARLY; -1: default)
-    int fuseHold = -1;       // hold workgroups (env MAS_FUSE_HOLD; -1: the resident slots)
-    int fuseSlots = 0;       // resident k_apply_fused workgroups on the chip
-    unsigned long long fuseApplies = 0;  // fused applies since the tables were built
     unsigned coarse1Epoch = 0;
     int c1PollDelay = 0;  // A/B (env MAS_C1_POLL_DELAY): fold / solve waves sleep before their first poll
     // bank waves of the one-launch coarse form dealt to the XCDs in contiguous
@@ -369,7 +362,7 @@ struct mas_context {
                               &tab, &termCnt,
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cdEnt, &c0Ent, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
-                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &tZ, &fuseDef, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart, &rsKeysP, &rsValsP, &rsHistP, &rsPartP, &add0, &c0Cnt, &c0Off, &c0Keys, &c0KeysS, &c0Ids, &c0IdsS,
                               &c0Val, &a0Keys, &a0KeysS, &a0Ids, &a0IdsS, &a0Val,
                               &spCst, &spGn, &spVmap, &spCoarseTables, &spFine, &spCoarseMask, &hierFlags, &recRanges,
@@ -441,9 +434,6 @@ void launch_coarse_twopass(mas_context* h, const float4* r, hipStream_t s);
 void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s);  // k_coarse1.hip (L >= 3)
 int build_coarse1_tables(mas_context* h, hipStream_t s);
 bool coarse1_supported(const mas_context* h);  // the tag slots exist (k_coarse1.hip)
-// the fused apply (coarse levels + level-0 blocks in one launch, k_coarse1.hip)
-bool fused_supported(const mas_context* h);
-void launch_apply_fused(mas_context* h, const float4* r, float4* z, hipStream_t s);
 void launch_coarse_levels(mas_context* h, int lFirst, const float4* d_r, hipStream_t s);
 void launch_coarse_deep(mas_context* h, const float4* src, const int* idx, hipStream_t s);
 int deep_nodes(const mas_context* h);  // level-3 node ids incl. padding (0 below L = 4)
