@@ -440,6 +440,39 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_true_finish(const double* _
     if (threadIdx.x == 0) st->rrTrue = rr;
 }
 
+struct PDecision {
+    bool stop;
+    float beta;
+};
+// The end of iteration it (every workgroup takes the same decision from the
+// same partials; workgroup 0 records it): the stop test and beta.
+__device__ __forceinline__ PDecision p_decision(int it, PcgState* __restrict__ st, const double* __restrict__ part,
+                                                const double* __restrict__ rzPart, int nRz) {
+    double rr = sum_partials(part + kPartRR * kPcgBlocks);
+    const double lim = st->tol2 * st->bb;
+    const bool replaced = rr <= lim;
+    if (replaced) rr = sum_partials(part + kPartRRX * kPcgBlocks);
+    const bool stop = (replaced && rr <= lim) || it + 1 >= st->maxIters;
+    const double rzOld = st->rz[it & 1];
+    const double rzNew = sum_partials(rzPart, nRz);
+    __syncthreads();  // every thread has read st before workgroup 0 writes it
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->rr = rr;
+        st->iters = it + 1;
+        st->rz[(it + 1) & 1] = rzNew;
+        if (replaced) {
+            if (st->firstPass == 0) st->firstPass = it + 1;
+            st->replacements++;
+        }
+        if (stop) st->done = 1;
+    }
+    return PDecision{stop, (float)(rzNew / rzOld)};
+}
+
+__device__ __forceinline__ float4 p_next(float beta, float4 pv, float4 zv) {
+    return make_float4(__fmaf_rn(beta, pv.x, zv.x), __fmaf_rn(beta, pv.y, zv.y), __fmaf_rn(beta, pv.z, zv.z), 0.f);
+}
+
 // Ap = A p; partials p.Ap
 #ifndef MAS_SPMV_PIPE
 #define MAS_SPMV_PIPE 1
@@ -459,15 +492,31 @@ __device__ __forceinline__ void ell_load(int g0, int lane, const float* __restri
     for (int q = 0; q < 9; ++q) e.m[q] = __builtin_nontemporal_load(ellOff + (size_t)g0 * 576 + q * 64 + lane);
 }
 
-template <int G>
+// FUSE (MAS_PCG_FUSE_P, the default): the previous iteration's update_p
+// inside this launch -- its stop decision and beta (p_decision), and
+// p = z + beta p_old evaluated wherever a p entry is read (each neighbour's
+// too: the same fma on the same inputs, so the same bits as the stored p of
+// the unfused form); every row stores its own p into pOut (p_old stays
+// intact for the other rows' gathers).  One launch and one pass over z and p
+// less per iteration; the iterates are bitwise those of the unfused form.
+template <int G, bool FUSE>
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __restrict__ starts,
                                                           const int* __restrict__ idx, const float* __restrict__ diag,
                                                           const float* __restrict__ off,
                                                           const float* __restrict__ ellOff,
                                                           const int* __restrict__ ellIdx, const float4* __restrict__ p,
-                                                          float4* __restrict__ ap, const PcgState* __restrict__ st,
-                                                          double* __restrict__ part) {
+                                                          float4* __restrict__ ap, PcgState* __restrict__ st,
+                                                          double* __restrict__ part, const float4* __restrict__ zf,
+                                                          float4* __restrict__ pOut, const double* __restrict__ rzPart,
+                                                          int nRz, int itPrev) {
     if (st->done) return;
+    float beta = 0.f;
+    if (FUSE) {
+        const PDecision d = p_decision(itPrev, st, part, rzPart, nRz);
+        if (d.stop) return;
+        beta = d.beta;
+    }
+    auto pv = [&](int j) { return FUSE ? p_next(beta, p[j], zf[j]) : p[j]; };
     const int lane = threadIdx.x & 63, sub = lane % G;
     constexpr int rowsPerWave = kSpmvRows * (64 / G);
     XcdRows xr(nV, rowsPerWave);
@@ -487,8 +536,8 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __r
             const int v = base + lane / G;
             const bool valid = v < nV;
             const int vc = valid ? v : 0;
-            const float4 xn = p[cur.nb >= 0 ? cur.nb : 0];
-            const float4 xd = p[vc];
+            const float4 xn = pv(cur.nb >= 0 ? cur.nb : 0);
+            const float4 xd = pv(vc);
             const int e = starts[vc] + sub, e1 = valid ? starts[vc + 1] : 0;
             float dg[9];
             __builtin_memcpy(dg, diag + 9 * (size_t)vc, 36);
@@ -499,7 +548,7 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __r
             float3 withN = acc;
             add3(withN, mat3_mul(cur.m, xn));
             if (cur.nb >= 0) acc = withN;
-            for (int ee = e + G; ee < e1; ee += G) add3(acc, mat3_mul(off + 9 * (size_t)ee, p[idx[ee]]));
+            for (int ee = e + G; ee < e1; ee += G) add3(acc, mat3_mul(off + 9 * (size_t)ee, pv(idx[ee])));
 #pragma unroll
             for (int o = G / 2; o > 0; o >>= 1) {
                 acc.x = __fadd_rn(acc.x, __shfl_xor(acc.x, o));
@@ -508,6 +557,7 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __r
             }
             if (sub == 0 && valid) {
                 ap[v] = make_float4(acc.x, acc.y, acc.z, 0.f);
+                if (FUSE) pOut[v] = xd;
                 pap += dot3(acc, xd);
             }
         };
@@ -521,6 +571,7 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __r
             base += xr.stride;
         }
     } else {
+        static_assert(!FUSE || (MAS_SPMV_PIPE && MAS_SPMV_NT && kSpmvRows == 1), "the fused p update needs the pipelined form");
         for (int base = xr.first; base < xr.end; base += xr.stride) {
             int v[kSpmvRows];
             float3 y[kSpmvRows];
@@ -593,30 +644,10 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update_p(int nV, int it, co
                                                               const double* __restrict__ part,
                                                               const double* __restrict__ rzPart, int nRz) {
     if (st->done) return;
-    double rr = sum_partials(part + kPartRR * kPcgBlocks);
-    const double lim = st->tol2 * st->bb;
-    const bool replaced = rr <= lim;
-    if (replaced) rr = sum_partials(part + kPartRRX * kPcgBlocks);
-    const bool stop = (replaced && rr <= lim) || it + 1 >= st->maxIters;
-    const double rzOld = st->rz[it & 1];
-    const double rzNew = sum_partials(rzPart, nRz);
-    __syncthreads();  // every thread has read st before workgroup 0 writes it
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->rr = rr;
-        st->iters = it + 1;
-        st->rz[(it + 1) & 1] = rzNew;
-        if (replaced) {
-            if (st->firstPass == 0) st->firstPass = it + 1;
-            st->replacements++;
-        }
-        if (stop) st->done = 1;
-    }
-    if (stop) return;
-    const float beta = (float)(rzNew / rzOld);
-    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads) {
-        const float4 zv = z[v], pv = p[v];
-        p[v] = make_float4(__fmaf_rn(beta, pv.x, zv.x), __fmaf_rn(beta, pv.y, zv.y), __fmaf_rn(beta, pv.z, zv.z), 0.f);
-    }
+    const PDecision d = p_decision(it, st, part, rzPart, nRz);
+    if (d.stop) return;
+    for (int v = blockIdx.x * kPcgThreads + threadIdx.x; v < nV; v += kPcgBlocks * kPcgThreads)
+        p[v] = p_next(d.beta, p[v], z[v]);
 }
 
 // z = r (no preconditioner) with the r.z partials
@@ -643,6 +674,8 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     float4* p = z + nV;
     float4* ap = p + nV;
     X64* x64 = reinterpret_cast<X64*>(ap + nV);
+    float4* p2 = reinterpret_cast<float4*>(x64 + nV);  // the fused form's p of odd iterations
+    const bool fuseP = h->pcgFuseP;
     double* part = P<double>(h->pcgPartial);
     const int* idx = P<int>(h->idx);
     const dim3 g(kPcgBlocks), b(kPcgThreads);
@@ -690,17 +723,26 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     int pendingSeq = 0;
     bool pending = false;
     const int chunk = 4;
+    int lastK = -1;
     for (int it = 0; it < maxIters; it += chunk) {
         for (int k = it; k < it + chunk && k < maxIters; ++k) {
-            k_pcg_spmv<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, p, ap, st, part);
-            k_pcg_update_xr<<<g, b, 0, s>>>(nV, k, p, ap, x64, r, st, part);
+            // the fused form: iteration k's p lives in (k even ? p : p2), formed by this SpMV from the last
+            float4* pk = fuseP && (k & 1) ? p2 : p;
+            if (!fuseP || k == 0)
+                k_pcg_spmv<G, false><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, pk, ap, st,
+                                                     part, nullptr, nullptr, nullptr, 0, 0);
+            else
+                k_pcg_spmv<G, true><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx,
+                                                    (k & 1) ? p : p2, ap, st, part, z, pk, rzPart, nRz, k - 1);
+            k_pcg_update_xr<<<g, b, 0, s>>>(nV, k, pk, ap, x64, r, st, part);
             k_pcg_true<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, x64, d_b, r, st, part);
             if (precondition) {
                 if ((rc = run_apply(h, z, r, s))) return rc;
             } else {
                 k_pcg_copy<<<g, b, 0, s>>>(nV, r, z, st, rzPart);
             }
-            k_pcg_update_p<<<g, b, 0, s>>>(nV, k, z, p, st, part, rzPart, nRz);
+            if (!fuseP) k_pcg_update_p<<<g, b, 0, s>>>(nV, k, z, p, st, part, rzPart, nRz);
+            lastK = k;
         }
         if (lag) {
             int seq = 0, done = 0;
@@ -718,6 +760,12 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
             return rc;
         if (host.done) break;
     }
+    // the fused form: the last queued iteration's stop decision (its update_p
+    // would have been the next SpMV); a finished solve returns at once
+    if (fuseP && lastK >= 0) {
+        float4* pk = (lastK & 1) ? p2 : p;
+        k_pcg_update_p<<<g, b, 0, s>>>(nV, lastK, z, pk, st, part, rzPart, nRz);
+    }
     k_pcg_xout<<<g, b, 0, s>>>(nV, x64, d_x);
     hipEventRecord(e1, s);
     // the true residual of the returned x (fp64 evaluation)
@@ -731,7 +779,7 @@ int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int
     const int nV = h->nV;
     int rc;
     if (precondition && (rc = pending_giveup(h))) return rc;  // an earlier apply's incomplete z, first
-    if ((rc = ensure(h, h->pcgVec, (size_t)nV * (16 * 4 + sizeof(X64)))) ||
+    if ((rc = ensure(h, h->pcgVec, (size_t)nV * (16 * 5 + sizeof(X64)))) ||
         (rc = ensure(h, h->pcgPartial, (size_t)kPcgBlocks * kParts * sizeof(double))) ||
         (rc = ensure(h, h->pcgState, sizeof(PcgState))))
         return rc;

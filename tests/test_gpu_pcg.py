@@ -128,3 +128,29 @@ def test_pcg_edge_cases():
     xs, rs = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=500, tol=TOL)
     x2, r2 = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, x0=xs, max_iters=500, tol=10 * TOL)
     assert r2["iterations"] <= 1
+
+
+@pytest.mark.parametrize("W,L,precondition,maxit", [(100, 3, True, 3000), (256, 4, True, 3000), (100, 3, False, 3000),
+                                                    (100, 3, True, 7)])
+def test_pcg_fused_p_update_bitwise(W, L, precondition, maxit, monkeypatch):
+    """p = z + beta p inside the next SpMV (MAS_PCG_FUSE_P=1, the default) and
+    as its own pass (0): the same iterates bit for bit -- x, the iteration
+    counts, the replacements, the residuals -- also when max_iters stops the
+    solve (the last decision then runs after the loop)."""
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(W)
+    b = meshgen.residual(mesh.nV, 11)
+    out = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("MAS_PCG_FUSE_P", fuse)
+        P = mas_amd.from_mesh(mesh, max_levels=L)
+        x, res = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=maxit, tol=TOL,
+                             precondition=precondition)
+        out.append((x, res))
+    (x0, r0), (x1, r1) = out
+    assert np.array_equal(x0.view(np.uint32), x1.view(np.uint32))
+    for k in ("iterations", "converged", "replacements", "first_pass_iterations", "rel_residual", "true_rel_residual"):
+        assert r0[k] == r1[k], (k, r0[k], r1[k])
+    if maxit == 7:
+        assert r1["iterations"] == 7 and not r1["converged"]
