@@ -108,7 +108,6 @@ struct Coarse1Args {
     int* timeouts;        // waits that gave up: this apply's z is incomplete (mas_stats.wait_timeouts)
     int* giveupHost;      // pinned host word: the epoch of an apply whose wait gave up (the next call reports it)
     const int2* members;  // grouped level 3: per coarse node (child bank, child mask); null: the reference's fold
-    int fold3InSolve;     // grouped level 3: the level-3 solve waves fold R3 (no fold waves, one hand-off less)
 };
 
 // A bounded wait gave up: count it on the device (mas_stats.wait_timeouts) and
@@ -352,65 +351,6 @@ __device__ __forceinline__ void solve_wave(const Coarse1Args& a, int blk, int lv
     C1_STAMP(2, slot, 2);
 }
 
-// grouped level 3 in the solve wave itself (one hand-off less on the chain):
-// lane 32 h + n polls children 16 h .. 16 h + 15 of level-3 node n of block
-// blk (the lanes of one component of one level-2 bank, members), folds R3 =
-// its children's R2 in lane (= level-2 id) order from +0 -- lane n its own 16,
-// then lane n + 32's 16 -- bitwise fold_wave_grouped's sum, then Z3 = Inv R3
-__device__ __forceinline__ void solve3_grouped(const Coarse1Args& a, int blk, int slot) {
-    const int lane = threadIdx.x & 63, n = lane & 31, hh = lane >> 5;
-    C1_STAMP(2, slot, 0);
-    float g[kRecord], tl[3];
-    load_record<true>(a.inv, blk, lane, g, tl);  // in flight during the polls
-    const int T = blk * 32 + n - a.lv3Begin;
-    const bool real = T < a.n3;
-    const int2 mb = real ? a.members[a.lv3Begin + T - a.begin1] : make_int2(0, 0);
-    const unsigned msk = ((unsigned)mb.y >> (16 * hh)) & 0xFFFFu;
-    const Tag3* src = a.tR2 + mb.x * 32 + 16 * hh;
-    unsigned long long v[16][3];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i][0] = v[i][1] = v[i][2] = 0ull;
-    unsigned pending = msk;
-    for (int polls = 0; polls <= a.pollLimit; ++polls) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if ((pending >> i) & 1u) {
-                ld_tag(src + i, v[i]);
-                if (tag_ok(v[i], a.epoch)) pending &= ~(1u << i);
-            }
-        if (__all(pending == 0u)) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    if (!__all(pending == 0u) && lane == 0) gave_up(a);  // R3 from stale R2: counted
-    C1_STAMP(2, slot, 1);
-    float x[16], y[16], z[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const bool in = (msk >> i) & 1u;
-        x[i] = in ? tag_val(v[i][0]) : 0.f;
-        y[i] = in ? tag_val(v[i][1]) : 0.f;
-        z[i] = in ? tag_val(v[i][2]) : 0.f;
-    }
-    float ax = 0.f, ay = 0.f, az = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        ax = __fadd_rn(ax, x[i]);
-        ay = __fadd_rn(ay, y[i]);
-        az = __fadd_rn(az, z[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        ax = __fadd_rn(ax, __shfl_xor(x[i], 32));
-        ay = __fadd_rn(ay, __shfl_xor(y[i], 32));
-        az = __fadd_rn(az, __shfl_xor(z[i], 32));
-    }
-    if (lane < 32 && real) a.rc[a.lv3Begin + T - a.begin1] = make_float4(ax, ay, az, 0.f);
-    // half 1 takes node n's residual from lane n (padding nodes: +0)
-    const float3 out = block_solve(g, tl, make_float3(__shfl(ax, n), __shfl(ay, n), __shfl(az, n)), lane);
-    if (lane < 32) a.zc[blk * 32 + n - a.begin1] = make_float4(out.x, out.y, out.z, 0.f);
-    C1_STAMP(2, slot, 2);
-}
-
 // grid (single-wave workgroups): [0, nb1) banks, then n3 fold waves, then nb2
 // level-2 and nb3 level-3 solve waves
 __global__ __launch_bounds__(64) void k_coarse1(Coarse1Args a) {
@@ -422,12 +362,6 @@ __global__ __launch_bounds__(64) void k_coarse1(Coarse1Args a) {
         return bank_wave(a, a.chunk && w < full ? (w & 7) * (full >> 3) + (w >> 3) : w, sh);
     }
     w -= a.nb1;
-    if (a.members && a.fold3InSolve) {  // grouped level 3 folded by the level-3 solve waves themselves
-        if (w < a.nb2) return solve_wave(a, a.lv2Begin / 32 + w, a.lv2Begin, a.n2, a.tR2, w);
-        w -= a.nb2;
-        if (w < a.nb3) solve3_grouped(a, a.lv3Begin / 32 + w, a.nb2 + w);
-        return;
-    }
     if (w < a.n3) return a.members ? fold_wave_grouped(a, w) : fold_wave(a, w, sh);
     w -= a.n3;
     if (w < a.nb2) return solve_wave(a, a.lv2Begin / 32 + w, a.lv2Begin, a.n2, a.tR2, w);
@@ -506,11 +440,10 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.done = h->applyDone;
     a.pollLimit = h->c1PollLimit;
     a.members = h->groupedR3 && deep ? P<int2>(h->members) : nullptr;
-    a.fold3InSolve = a.members && h->c1Fold3InSolve;
     a.timeouts = P<int>(h->devStatus) + 2;
     a.giveupHost = h->c1Host;
     h->c1Launched = true;
-    k_coarse1<<<a.nb1 + (a.fold3InSolve ? 0 : a.n3) + a.nb2 + a.nb3, 64, 0, s>>>(a);
+    k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3, 64, 0, s>>>(a);
     // mas_get_stats waits for this event (the latest one-launch apply, on
     // whatever stream it ran), not for the whole device; run_apply never
     // launches this form on a capturing stream

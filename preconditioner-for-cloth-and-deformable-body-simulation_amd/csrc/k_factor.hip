@@ -604,381 +604,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     factor_tiles<MFMA>(v, M, piv, dinv, inv + (size_t)blk * kBlockFloats, tileSlot, valuSlot, t, status, blk);
 }
 
-// ---------------------------------------------------------------------------
-// Two waves per block (MAS_FACTOR_WAVES=2): the same operations as
-// k_factor_fused, split over a 128-thread workgroup
-// ---------------------------------------------------------------------------
-//
-// k_factor_fused keeps a whole 96x96 block in one wave's registers (144 tile
-// VGPRs): two waves per SIMD, and each of the 96 elimination steps is a
-// dependent chain (pivot row through LDS, quad broadcasts, IEEE divisions,
-// FMAs) that those two waves cannot hide (~15 % of the VALU rate).  Here wave
-// w holds the row groups m = w, w + 2, w + 4 (rows rg + 16 m: the two waves'
-// rows interleave, so both stay busy until the last pivots): 72 tile VGPRs,
-// four waves per SIMD, and each step's FMAs are split over two SIMDs.  The
-// pivot row goes through a double-buffered LDS row and one workgroup barrier
-// per step.  Every element sees the reference's operations in the reference's
-// order: inverses bitwise equal to k_factor_fused's.
-template <int X>
-__device__ __forceinline__ void rb2_step(float (&v)[3][24], float* piv, float* dinv, int rg, int cg, int w) {
-    constexpr int mX = X / 16, rX = X % 16, cgX = X / 24, cX = X % 24;
-    constexpr int mLo = (X < 15) ? 0 : (X - 15) / 16 + 1;
-    constexpr int iX = mX >> 1, owner = mX & 1;
-    float* pr = piv + 96 * (X & 1);  // double-buffered: one barrier per step
-    if (w == owner && rg == rX) {
-#pragma unroll
-        for (int c4 = 0; c4 < 6; ++c4)
-            *reinterpret_cast<float4*>(&pr[24 * cg + 4 * c4]) =
-                make_float4(v[iX][4 * c4], v[iX][4 * c4 + 1], v[iX][4 * c4 + 2], v[iX][4 * c4 + 3]);
-    }
-    __syncthreads();
-    const float pd = pr[X];
-    {
-        const float d = __fdiv_rn(1.0f, pd);
-        if (w == 0 && rg == 0 && cg == 0) dinv[X] = d;
-    }
-    // local group i (m = 2 i + w) takes part when some row rg + 16 m > X
-    const int iLo = mLo <= w ? 0 : (mLo - w + 1) >> 1;  // first local group with m >= mLo
-    if (iLo > 2) return;
-    float a[3], r[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) a[i] = quad_bcast(v[i][cX], cgX);
-    // lane cg divides for local group i = cg
-    float q0 = 0.f;
-    {
-        float a0 = 0.f;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) a0 = (i == cg) ? a[i] : a0;
-        const int m0 = 2 * cg + w;
-        const bool act0 = cg < 3 && cg >= iLo && rg + 16 * m0 > X && a0 != 0.0f;
-        if (act0) q0 = __fdiv_rn(-a0, pd);
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) r[i] = quad_bcast(q0, i);
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-        float p[12];
-#pragma unroll
-        for (int c4 = 0; c4 < 3; ++c4) {
-            const float4 q = *reinterpret_cast<const float4*>(&pr[24 * cg + 12 * hh + 4 * c4]);
-            p[4 * c4] = q.x;
-            p[4 * c4 + 1] = q.y;
-            p[4 * c4 + 2] = q.z;
-            p[4 * c4 + 3] = q.w;
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-            if (i >= iLo)
-#pragma unroll
-                for (int c = 0; c < 12; ++c) v[i][12 * hh + c] = __fmaf_rn(r[i], p[c], v[i][12 * hh + c]);
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const bool upd = i >= iLo && (cg == cgX) && (rg + 16 * (2 * i + w) > X) && (a[i] != 0.0f);
-        v[i][cX] = upd ? r[i] : v[i][cX];
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int c = 0; c < 24; c += 2) {
-            v2f q = {v[i][c], v[i][c + 1]};
-            asm volatile("" : "+v"(q));
-            v[i][c] = q.x;
-            v[i][c + 1] = q.y;
-        }
-}
-
-template <int X>
-struct ElimRB2 {
-    static __device__ __forceinline__ void run(float (&v)[3][24], float* piv, float* dinv, int rg, int cg, int w) {
-        rb2_step<X>(v, piv, dinv, rg, cg, w);
-        ElimRB2<X + 1>::run(v, piv, dinv, rg, cg, w);
-    }
-};
-template <>
-struct ElimRB2<96> {
-    static __device__ __forceinline__ void run(float (&)[3][24], float*, float*, int, int, int) {}
-};
-
-// The slab of 16 nodes (48 rows) of half H, built by both waves: contacts by
-// wave 0 (as build_slab), the CSR terms of nodes 8 w .. 8 w + 7 by wave w
-// (each entry belongs to one node's rows, so the waves never add to the same
-// entry; within a node the slots add in ELL order as in build_slab).
-template <int H>
-__device__ __forceinline__ void build_slab2(const FineAsm& a, int blk, float* S, int w, int lane) {
-    const int tid = threadIdx.x;
-    float4* S4 = reinterpret_cast<float4*>(S);
-    for (int q = tid; q < 48 * 96 / 4; q += 128) S4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    __syncthreads();
-    if (a.coff) {
-        float* stg = S + 48 * 96;
-        const int q = lane < 9 ? lane : 0, qr = q % 3, qc = q / 3;
-        const int j0 = a.coff[blk], j1 = a.coff[blk + 1];
-        for (int jb = j0; jb < j1; jb += 16) {
-            const int cnt = min(16, j1 - jb);
-            if (w == 0 && lane < cnt) {
-                const int id = a.cids[jb + lane];
-                stg[10 * lane] = __int_as_float(a.cent[id]);
-                const float* src = a.cvals + 9 * (size_t)id;
-#pragma unroll
-                for (int e = 0; e < 9; ++e) stg[10 * lane + 1 + e] = src[e];
-            }
-            __syncthreads();
-            if (w == 0 && lane < 9)
-                for (int k = 0; k < cnt; ++k) {
-                    const int ent = __float_as_int(stg[10 * k]);
-                    const int nl = (ent >> 5) - 16 * H, col = ent & 31;
-                    if (nl >= 0 && nl < 16) {
-                        float* p = S + (3 * nl + qr) * 96 + 3 * col + qc;
-                        *p = __fadd_rn(*p, stg[10 * k + 1 + q]);
-                    }
-                }
-            __syncthreads();
-        }
-    }
-    // CSR terms: lane = (node n = 8 w + lane % 8, slot group g = lane / 8),
-    // ELL slot k = k0 + g + 8 p; a pass loads 2 slots per lane, then adds them in slot order
-    const int n = 8 * w + (lane & 7), g = lane >> 3;
-    const int v = 32 * blk + 16 * H + n;
-    const bool live = v < a.nV;
-    int o = 0, num = 0, base = 0;
-    if (live) {
-        o = a.s2o[v];
-        num = a.nbrNum[v];
-        base = a.ranges[o];
-    }
-    for (int k0 = 0; k0 < a.maxNbr; k0 += 16) {
-        float m[2][9];
-        int col[2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int k = k0 + g + 8 * p;
-            col[p] = -1;
-            if (!live || k >= num) continue;
-            if (k == 0) {  // diag (column-major) + additional (row-major), .cpp:1270
-                const float* d = a.diag9 + 9 * (size_t)o;
-                const float* ad = a.additional + 9 * (size_t)v;
-#pragma unroll
-                for (int r = 0; r < 3; ++r)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) m[p][r * 3 + c] = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);
-                col[p] = 16 * H + n;
-            } else {
-                const unsigned ot = (unsigned)a.nbr[(size_t)k * a.nV + v];
-                if ((ot >> 5) != ((unsigned)v >> 5)) continue;  // cross-bank: a coarse record
-                const float* src = a.off9 + 9 * ((size_t)base + k - 1);
-#pragma unroll
-                for (int r = 0; r < 3; ++r)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) m[p][r * 3 + c] = src[c * 3 + r];
-                col[p] = (int)(ot & 31);
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int gg = 0; gg < 8; ++gg)  // slot order within the vertex
-                if (g == gg && col[p] >= 0) {
-                    float* e = S + (3 * n) * 96 + 3 * col[p];
-#pragma unroll
-                    for (int r = 0; r < 3; ++r)
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], m[p][r * 3 + c]);
-                }
-    }
-    __syncthreads();
-    if (w == 0 && lane < 16) {  // zero diagonal -> identity node block (.cpp:1365-1368)
-        float* e = S + (3 * lane) * 96 + 3 * (16 * H + lane);
-        if (*e == 0.0f)
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) e[r * 96 + c] = (r == c) ? 1.f : 0.f;
-    }
-    __syncthreads();
-    if (a.keep) {
-        float4* dst = reinterpret_cast<float4*>(a.keep + (size_t)blk * kDenseFloats + 48 * 96 * H);
-        for (int q = tid; q < 48 * 96 / 4; q += 128) dst[q] = S4[q];
-    }
-}
-
-// rows of slab H into wave w's tiles: local group i holds m = 2 i + w
-template <int H>
-__device__ __forceinline__ void slab_to_tiles2(float (&v)[3][24], const float* S, int w, int lane) {
-    const int rg = lane >> 2, cg = lane & 3;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int m = 2 * i + w;
-        if (m < 3 * H || m >= 3 * H + 3) continue;  // wave-uniform
-#pragma unroll
-        for (int c4 = 0; c4 < 6; ++c4) {
-            const float4 q = *reinterpret_cast<const float4*>(&S[(rg + 16 * (m - 3 * H)) * 96 + 24 * cg + 4 * c4]);
-            v[i][4 * c4] = q.x;
-            v[i][4 * c4 + 1] = q.y;
-            v[i][4 * c4 + 2] = q.z;
-            v[i][4 * c4 + 3] = q.w;
-        }
-    }
-}
-
-// form_mfma split over the two waves: wave 0 the tiles (0,0) (0,2) (1,2),
-// wave 1 (0,1) (1,1) (2,2) -- 80 MFMAs each
-__device__ __forceinline__ void form_mfma2(float* M, const float* dinv, float* out, const uint4* __restrict__ tileSlot,
-                                           int w, int lane) {
-    const int col = lane & 31, kh = lane >> 5;
-    const int tI0[3] = {0, 0, 1}, tJ0[3] = {0, 2, 2}, tN0[3] = {0, 3, 4};
-    const int tI1[3] = {0, 1, 2}, tJ1[3] = {1, 1, 2}, tN1[3] = {1, 2, 5};
-    uint4 sl[6];
-    v16f acc[3];
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-        const int tn = w ? tN1[u] : tN0[u];
-        sl[2 * u] = tileSlot[(2 * tn) * 64 + lane];
-        sl[2 * u + 1] = tileSlot[(2 * tn + 1) * 64 + lane];
-        acc[u] = mfma_tile(M, dinv, w ? tI1[u] : tI0[u], w ? tJ1[u] : tJ0[u], col, kh);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();  // both waves done with M before it is overwritten
-    float* O = M;
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint4 wd = sl[2 * u + (r >> 3)];
-            const int h = (r & 7) >> 1;
-            const unsigned word = h == 0 ? wd.x : h == 1 ? wd.y : h == 2 ? wd.z : wd.w;
-            const unsigned slot = (r & 1) ? word >> 16 : word & 0xFFFFu;
-            if (slot != 0xFFFFu) O[slot] = acc[u][r];
-        }
-    __syncthreads();
-    const float4* O4 = reinterpret_cast<const float4*>(O);
-    float4* out4 = reinterpret_cast<float4*>(out);
-    for (int q = threadIdx.x; q < kBlockF4; q += 128) out4[q] = O4[q];
-}
-
-// form_packed_staged split over the two waves: tile = 64 (2 tt + w) + lane
-__device__ __forceinline__ void form_packed_staged2(float* M, const float* dinv, float* out,
-                                                    const uint4* __restrict__ valuSlot, int w, int lane) {
-    float acc[3][4][4];
-#pragma unroll
-    for (int tt = 0; tt < 3; ++tt) {
-        const int tile = 64 * (2 * tt + w) + lane;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) acc[tt][a][b] = 0.f;
-        if (tile >= 300) continue;
-        int J = 0, rem = tile;
-        while (rem > J) { rem -= J + 1; ++J; }
-        const int I = rem;
-        for (int k = 95; k >= 4 * J + 3; --k) {
-            const int base = m_row(k);
-            const float4 mi = *reinterpret_cast<const float4*>(&M[base + 4 * I]);
-            const float4 mj = *reinterpret_cast<const float4*>(&M[base + 4 * J]);
-            const float d = dinv[k];
-            const float fi[4] = {mi.x, mi.y, mi.z, mi.w}, fj[4] = {mj.x, mj.y, mj.z, mj.w};
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b) acc[tt][a][b] = __fmaf_rn(d, __fmul_rn(fi[a], fj[b]), acc[tt][a][b]);
-        }
-#pragma unroll
-        for (int kk = 2; kk >= 0; --kk) {
-            const int k = 4 * J + kk, base = m_row(k);
-            const float4 mi = *reinterpret_cast<const float4*>(&M[base + 4 * I]);
-            const float4 mj = *reinterpret_cast<const float4*>(&M[base + 4 * J]);
-            const float d = dinv[k];
-            const float fi[4] = {mi.x, mi.y, mi.z, mi.w}, fj[4] = {mj.x, mj.y, mj.z, mj.w};
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b <= kk; ++b) acc[tt][a][b] = __fmaf_rn(d, __fmul_rn(fi[a], fj[b]), acc[tt][a][b]);
-        }
-    }
-    uint4 sl[6];
-#pragma unroll
-    for (int tt = 0; tt < 3; ++tt) {
-        const int t0 = 64 * (2 * tt + w) + lane, tile = t0 < 300 ? t0 : 0;
-        sl[2 * tt] = valuSlot[2 * tile];
-        sl[2 * tt + 1] = valuSlot[2 * tile + 1];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    float* O = M;
-#pragma unroll
-    for (int tt = 0; tt < 3; ++tt) {
-        if (64 * (2 * tt + w) + lane >= 300) continue;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const uint4 wd = sl[2 * tt + (e >> 3)];
-            const int h = (e & 7) >> 1;
-            const unsigned word = h == 0 ? wd.x : h == 1 ? wd.y : h == 2 ? wd.z : wd.w;
-            const unsigned slot = (e & 1) ? word >> 16 : word & 0xFFFFu;
-            if (slot != 0xFFFFu) O[slot] = acc[tt][e >> 2][e & 3];
-        }
-    }
-    __syncthreads();
-    const float4* O4 = reinterpret_cast<const float4*>(O);
-    float4* out4 = reinterpret_cast<float4*>(out);
-    for (int q = threadIdx.x; q < kBlockF4; q += 128) out4[q] = O4[q];
-}
-
-template <bool MFMA>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_factor_fused2(
-    FineAsm a, float* __restrict__ inv, const uint4* __restrict__ tileSlot, const uint4* __restrict__ valuSlot,
-    int blk0, int* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) float M[kPackedM];
-    __shared__ __attribute__((aligned(16))) float piv[2 * 96];
-    __shared__ float dinv[96];
-    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
-    const int rg = t >> 2, cg = t & 3;
-    const int blk = blk0 + blockIdx.x;
-    float v[3][24];
-    build_slab2<0>(a, blk, M, w, t);
-    slab_to_tiles2<0>(v, M, w, t);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab 0 read before slab 1 overwrites it
-    __syncthreads();
-    build_slab2<1>(a, blk, M, w, t);
-    slab_to_tiles2<1>(v, M, w, t);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    ElimRB2<0>::run(v, piv, dinv, rg, cg, w);
-    // M rows of this wave's groups: unit diagonal, L^-1 below
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int k = rg + 16 * (2 * i + w), len = (k & ~3) + 4;
-#pragma unroll
-        for (int c4 = 0; c4 < 6; ++c4) {
-            const int col = 24 * cg + 4 * c4;
-            if (col < len) {
-                float4 q = make_float4(v[i][4 * c4], v[i][4 * c4 + 1], v[i][4 * c4 + 2], v[i][4 * c4 + 3]);
-                if (col == (k & ~3)) {
-                    const int d = k & 3;
-                    q.x = d == 0 ? 1.f : q.x;
-                    q.y = d == 1 ? 1.f : q.y;
-                    q.z = d == 2 ? 1.f : q.z;
-                    q.w = d == 3 ? 1.f : q.w;
-                }
-                *reinterpret_cast<float4*>(&M[m_row(k) + col]) = q;
-            }
-        }
-    }
-    __syncthreads();
-    if (status && w == 0) check_pivots(dinv, status, blk, t);
-    float* out = inv + (size_t)blk * kBlockFloats;
-    if (MFMA) form_mfma2(M, dinv, out, tileSlot, w, t);
-    else form_packed_staged2(M, dinv, out, valuSlot, w, t);
-}
-
+// (A two-wave-per-block form of this kernel -- wave w holding the row groups
+// m = w, w + 2, w + 4, the pivot row through a double-buffered LDS row and one
+// workgroup barrier per step -- was bitwise equal but slower, 2.18 -> 2.75 ms
+// at 1M + contacts: LDS and VGPRs already allow 8 blocks per CU either way,
+// so it only added a barrier to every step; profiles/round5/ab/.)
 int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s) {
-    // MAS_FACTOR_VARIANT=5: the matrix-core formation (form_mfma, not bitwise);
-    // MAS_FACTOR_WAVES=2: two waves per block (k_factor_fused2)
-    if (blk1 > blk0 && h->factorWaves == 2) {
-        if (h->factorVariant == 5)
-            k_factor_fused2<true><<<blk1 - blk0, 128, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
-                                                             P<uint4>(h->valuSlot), blk0, P<int>(h->devStatus));
-        else
-            k_factor_fused2<false><<<blk1 - blk0, 128, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
-                                                              P<uint4>(h->valuSlot), blk0, P<int>(h->devStatus));
-    } else if (blk1 > blk0 && h->factorVariant == 5)
+    // MAS_FACTOR_VARIANT=5: the matrix-core formation (form_mfma, not bitwise)
+    if (blk1 > blk0 && h->factorVariant == 5)
         k_factor_fused<true><<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
                                                         P<uint4>(h->valuSlot), blk0, P<int>(h->devStatus));
     else if (blk1 > blk0)

@@ -194,13 +194,11 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     h->groupedR3 = !h->cfg.reference_restriction;
     if (const char* v = std::getenv("MAS_REF_RESTRICT")) h->groupedR3 = !std::atoi(v);
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
-    if (const char* v = std::getenv("MAS_FACTOR_WAVES")) h->factorWaves = std::atoi(v);
     if (const char* v = std::getenv("MAS_PCG_FUSE_P")) h->pcgFuseP = std::atoi(v) != 0;
     if (const char* v = std::getenv("MAS_COARSE_MODE")) h->coarseMode = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_POLL_DELAY")) h->c1PollDelay = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_CHUNK")) h->c1Chunk = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_POLL_LIMIT")) h->c1PollLimit = std::atoi(v);
-    if (const char* v = std::getenv("MAS_C1_FOLD3")) h->c1Fold3InSolve = std::atoi(v);
     if (const char* v = std::getenv("MAS_PREP_CU_RESERVE")) h->prepCuReserve = std::atoi(v);
     if (const char* v = std::getenv("MAS_FUSED_AFTER_LEVELS")) h->fusedAfterLevels = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_THREAD")) h->earlyThread = std::atoi(v);

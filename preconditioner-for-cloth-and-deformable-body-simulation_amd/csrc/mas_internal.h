@@ -176,7 +176,6 @@ struct mas_context {
     // formation (not bitwise, the default; mas_config.reference_formation = 1
     // selects 4); 0 = LDS-row k_factor
     int factorVariant = 5;
-    int factorWaves = 1;  // waves per block of the fused level-0 factor (env MAS_FACTOR_WAVES: 1 or 2)
     // coarse levels (env MAS_COARSE_MODE): 3 = one launch with tagged
     // hand-offs (k_coarse1.hip, L >= 3); 2 = two launches, restrictions then
     // every solve (k_coarse.hip, L >= 3); 0 = one launch per level.  (The
@@ -301,9 +300,6 @@ struct mas_context {
     // k_coarse1's bounded waits never hang the device: a wait gives up after
     // this many polls and is counted (env MAS_C1_POLL_LIMIT; < 0 forces it: tests)
     int c1PollLimit = 1 << 16;
-    // grouped level 3: the level-3 solve waves poll the R2 of their nodes'
-    // children and fold R3 themselves, no fold waves (env MAS_C1_FOLD3=0: fold waves, A/B)
-    int c1Fold3InSolve = 1;
     bool c1Launched = false;    // k_coarse1 ran since the handle was created (evC1 has been recorded)
     hipEvent_t evC1 = nullptr;  // after the latest k_coarse1 launch (mas_get_stats waits for it)
     // pinned host-coherent word: the epoch of the latest apply whose k_coarse1
