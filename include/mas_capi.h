@@ -144,8 +144,8 @@ typedef struct {
     double prepare_fine_start_ms; /* the fused level-0 kernel's start, after the Prepare's start */
     int64_t nonspd_blocks;     /* the last Prepare: blocks whose factor met a zero / negative / non-finite pivot */
     int64_t wait_timeouts;     /* since mas_create: bounded device waits of the one-launch coarse form that
-                                  gave up (that apply's z is then incomplete), as of the latest such apply
-                                  (waits for it, not for the device).  The apply that gave up is named by
+                                  gave up (that apply's z is then incomplete), read on the handle's own
+                                  stream (no device-wide sync).  The apply that gave up is named by
                                   MAS_ERR_HIP from mas_apply / the PCG solve itself, or for mas_apply_device
                                   from the next mas_apply* / PCG call on the handle */
     int64_t reserved[3];       /* zero; room for later fields without a size change */

@@ -444,10 +444,9 @@ void launch_coarse_one(mas_context* h, const float4* r, hipStream_t s) {
     a.giveupHost = h->c1Host;
     h->c1Launched = true;
     k_coarse1<<<a.nb1 + a.n3 + a.nb2 + a.nb3, 64, 0, s>>>(a);
-    // mas_get_stats waits for this event (the latest one-launch apply, on
-    // whatever stream it ran), not for the whole device; run_apply never
-    // launches this form on a capturing stream
-    hipEventRecord(h->evC1, s);
+    // (no event here: a marker between k_coarse1 and the fine kernel held the
+    // fine kernel back ~5 us per apply -- the trace's coarse -> fine gap went
+    // from ~0 to 6.7 us; mas_get_stats reads the counter on its own stream)
 }
 
 

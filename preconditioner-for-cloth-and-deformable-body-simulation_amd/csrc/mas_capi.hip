@@ -177,8 +177,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     for (auto& e : h->ev) hipEventCreate(&e);
     {
         void* p = nullptr;
-        if (hipEventCreateWithFlags(&h->evC1, hipEventDisableTiming) != hipSuccess ||
-            hipHostMalloc(&p, 64, hipHostMallocCoherent) != hipSuccess) {
+        if (hipHostMalloc(&p, 64, hipHostMallocCoherent) != hipSuccess) {
             mas_destroy(h);
             return MAS_ERR_HIP;
         }
@@ -252,7 +251,6 @@ int mas_destroy(mas_handle h) {
     if (h->evShardDone) hipEventDestroy(h->evShardDone);
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->rbHost) hipHostFree(h->rbHost);
-    if (h->evC1) hipEventDestroy(h->evC1);
     if (h->c1Host) hipHostFree(h->c1Host);
     delete h;
     return MAS_OK;
@@ -446,13 +444,13 @@ int mas_get_stats(mas_handle h, mas_stats* out) {
     }
     h->stats.apply_mode = coarse_mode(h);
     if (h->c1Launched) {
-        // the waits that gave up, counted on the device since mas_create, as of
-        // the latest one-launch apply (on whatever stream it ran): waits for that
-        // apply's event and the handle's stream only, never the whole device
+        // the waits that gave up, counted on the device since mas_create, read
+        // on the handle's own stream: no device-wide synchronisation (applies
+        // still running on another stream may add to it later; each apply
+        // that gives up is also reported by the next call, pending_giveup)
         hipSetDevice(h->device);
         int n = 0;
-        if (hipEventSynchronize(h->evC1) != hipSuccess ||
-            hipMemcpyAsync(&n, P<int>(h->devStatus) + 2, 4, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        if (hipMemcpyAsync(&n, P<int>(h->devStatus) + 2, 4, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
             hipStreamSynchronize(h->stream) != hipSuccess)
             return fail(h, MAS_ERR_HIP, "mas_get_stats: reading the wait counter");
         h->stats.wait_timeouts = n;

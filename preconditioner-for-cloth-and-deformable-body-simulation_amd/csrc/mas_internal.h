@@ -300,8 +300,7 @@ struct mas_context {
     // k_coarse1's bounded waits never hang the device: a wait gives up after
     // this many polls and is counted (env MAS_C1_POLL_LIMIT; < 0 forces it: tests)
     int c1PollLimit = 1 << 16;
-    bool c1Launched = false;    // k_coarse1 ran since the handle was created (evC1 has been recorded)
-    hipEvent_t evC1 = nullptr;  // after the latest k_coarse1 launch (mas_get_stats waits for it)
+    bool c1Launched = false;    // k_coarse1 ran since the handle was created
     // pinned host-coherent word: the epoch of the latest apply whose k_coarse1
     // wait gave up, 0 when none since the last report (pending_giveup)
     int* c1Host = nullptr;
