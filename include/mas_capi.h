@@ -218,6 +218,14 @@ int mas_pcg_solve(mas_handle h, const float* diag9, const float* off9, const int
 /* Record HIP events around the apply kernels of every mas_apply_device call
  * (up to 4096 applies) and reset the averages in mas_stats. */
 int mas_set_profiling(mas_handle h, int enable);
+/* ABI 4.  Duration of the level-0 kernel of mas_apply_device alone (gather,
+ * block solves, prolongation from the coarse Z of the last apply): n
+ * back-to-back launches on `stream` between two HIP events, synchronised;
+ * *ms_per_launch = their average.  A timing marker between two kernels holds
+ * the second one back by several microseconds, so the per-apply events of
+ * mas_set_profiling overstate this kernel; back-to-back launches do not (the
+ * roofline source of bench.py).  d_z4 is written as by an apply. */
+int mas_profile_fine(mas_handle h, float* d_z4, const float* d_r4, int n, void* stream, double* ms_per_launch);
 
 /* ---- Morton-range sharding across `world` ranks (one process per GPU) ----
  * Rank g owns a contiguous range of level-0 blocks (equal split).  Clusters

@@ -402,3 +402,21 @@ def test_contact_records_validated_on_device():
     bad["fId"][123] = mesh.faces.shape[0] + 5
     with pytest.raises(mas_amd.MasError, match="out-of-range"):
         mas_amd.from_mesh(mesh, contacts=(bad, vfC))
+
+
+def test_profile_fine_writes_the_apply_z():
+    """mas_profile_fine (bench.py's roofline timing) launches the apply's own
+    level-0 kernel: after an apply, n back-to-back launches leave z bitwise as
+    the apply wrote it, and the reported duration is positive."""
+    import torch
+    from mas_amd import meshgen
+    mesh = cloth(256)
+    P = _gpu(mesh, 4, reference_formation=False)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 3)).cuda()
+    z1, z2 = torch.zeros_like(r), torch.full_like(r, float("nan"))
+    s = torch.cuda.Stream()
+    P.PreconditioningDevice(z1, r, s.cuda_stream)
+    ms = P.profile_fine(z2, r, 5, s.cuda_stream)
+    s.synchronize()
+    assert ms > 0
+    assert torch.equal(z1, z2)
