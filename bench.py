@@ -577,6 +577,11 @@ def main():
             dr = torch.from_numpy(np.ascontiguousarray(mesh.starts, np.int32)).cuda()
             torch.cuda.synchronize()
             pcg = {}
+            # one untimed solve first: a process's first solve also pays first-use
+            # costs (0.244 vs 0.234 ms/iteration at 1M + contacts, profiles/round5/ab/)
+            xw = torch.zeros_like(r)
+            P.pcg_solve_device(dd, do, dr, xw, r, max_iters=5000, tol=1e-5, precondition=True, stream=sptr)
+            torch.cuda.synchronize()
             for name, pre in (("mas", True), ("none", False)):
                 x = torch.zeros_like(r)
                 res = P.pcg_solve_device(dd, do, dr, x, r, max_iters=5000, tol=1e-5, precondition=pre,
@@ -585,7 +590,8 @@ def main():
                 pcg[name] = {k: (float(f"{v:.4g}") if isinstance(v, float) else v) for k, v in res.items()}
                 pcg[name]["ms_per_iter"] = round(res["solve_ms"] / max(res["iterations"], 1), 4)
             pcg["tol"] = 1e-5
-            pcg["note"] = "Prepare excluded; the contact stencils are in the preconditioner only (A = CSR Hessian)"
+            pcg["note"] = ("Prepare excluded; the contact stencils are in the preconditioner only (A = CSR Hessian); "
+                           "the second MAS solve of the process (one untimed solve first)")
             out["pcg_solve"] = pcg
         except Exception as e:  # context only
             log(f"pcg report failed: {e!r}")

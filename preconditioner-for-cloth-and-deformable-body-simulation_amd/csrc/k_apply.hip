@@ -276,9 +276,15 @@ __global__ __launch_bounds__(256) void k_members(int nChild, int childBegin, con
 template <int NPROL>
 static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int blk0, int blkEnd, int nV,
                           const float4* r, const int4* vmap, const float4* zc, int begin1, float4* z,
-                          const int* done, double* rzPart) {
+                          const int* done, double* rzPart, int rzWpb = 2) {
     if (rzPart) {  // the PCG driver's applies (fine_grid(h) workgroups: one r.z partial each)
-        if (var == 6)
+        if (var == 6 && rzWpb == 8)
+            k_solve_fine<NPROL, 4, true, 8><<<cdiv(blkEnd - blk0, 8), 512, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
+                                                                                 begin1, z, done, rzPart);
+        else if (var == 6 && rzWpb == 4)
+            k_solve_fine<NPROL, 4, true, 4><<<cdiv(blkEnd - blk0, 4), 256, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
+                                                                                 begin1, z, done, rzPart);
+        else if (var == 6)
             k_solve_fine<NPROL, 4, true, 2><<<cdiv(blkEnd - blk0, 2), 128, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
                                                                                  begin1, z, done, rzPart);
         else if (var == 0)
@@ -320,15 +326,19 @@ void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* 
     const int4* vmap = P<int4>(h->vmap);
     const float4* zc = P<float4>(h->Zc);
     const int begin1 = h->levelSize[3], nV = h->nV, var = h->fineVariant;
+    const int w = h->rzWpb;
     switch (L < 4 ? L - 1 : 3) {
-        case 0: launch_fine_n<0>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart); break;
-        case 1: launch_fine_n<1>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart); break;
-        case 2: launch_fine_n<2>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart); break;
-        default: launch_fine_n<3>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart); break;
+        case 0: launch_fine_n<0>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
+        case 1: launch_fine_n<1>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
+        case 2: launch_fine_n<2>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
+        default: launch_fine_n<3>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
     }
 }
 
-int fine_grid(const mas_context* h) { return cdiv(h->nFineBlk, h->fineVariant == 6 ? 2 : kApplyThreads / 64); }
+// workgroups of one fine launch of the PCG's applies (= its r.z partials)
+int fine_grid(const mas_context* h) {
+    return cdiv(h->nFineBlk, h->fineVariant == 6 ? h->rzWpb : kApplyThreads / 64);
+}
 
 // coarse levels lFirst..L-1: level 1 from the vertices (k_coarse_l1), level
 // 2 from R1 (k_coarse_up), levels >= 3 in one k_coarse_deep launch (R folded

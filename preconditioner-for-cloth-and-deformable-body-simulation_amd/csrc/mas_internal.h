@@ -197,6 +197,11 @@ struct mas_context {
     // chunking (A/B); 3 = 1 in one-wave workgroups (A/B); 0 = default-policy
     // loads (A/B)
     int fineVariant = 6;
+    // blocks (waves) per workgroup of the fine kernel in the PCG's applies,
+    // one r.z partial per workgroup, summed by every SpMV workgroup (env
+    // MAS_RZ_WPB: 2, 4 or 8): 4 measured 0.8-1.0 us per iteration faster
+    // than 2 at 1M + contacts, 8 17 us slower (profiles/round5/ab/pcg_rz_wpb.txt)
+    int rzWpb = 4;
     int totalClusters = 0, nBlk = 0, nFineBlk = 0, nStencil = 0;
     int nStencilEF = 0;  // of nStencil, the EF stencils (at most 5 vertices; EE / VF have 4)
     int nBlkPrev = 0;  // nBlk of the previous Prepare, read by the early path's thread (run_levels may change nBlk meanwhile)
