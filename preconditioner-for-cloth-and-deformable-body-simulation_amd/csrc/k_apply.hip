@@ -61,14 +61,14 @@ __device__ __forceinline__ void solve_fine_body(const float4* __restrict__ inv, 
                                                 const float4* __restrict__ zc, int begin1, float4* __restrict__ z,
                                                 double* __restrict__ rzPart) {
     const int lane = threadIdx.x & 63, n = lane & 31;
-    const int wg = VAR == 4 ? xcd_chunked(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int wg = (VAR == 4 || VAR == 8) ? xcd_chunked(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int blk = blk0 + wg * WPB + (threadIdx.x >> 6);
     const bool bvalid = blk < nFineBlk;
     const int v = blk * 32 + n;
     const bool vvalid = bvalid && v < nV;
     const int4 m = vmap[vvalid ? v : 0];
     float g[kRecord], tl[3];
-    load_record<VAR != 0>(inv, bvalid ? blk : 0, lane, g, tl);
+    load_record<VAR != 0 && VAR != 8>(inv, bvalid ? blk : 0, lane, g, tl);
     const float4 rv = r[m.x];
     const float3 rr = vvalid ? make_float3(rv.x, rv.y, rv.z) : make_float3(0.f, 0.f, 0.f);
     float3 out = block_solve(g, tl, rr, lane);
@@ -284,6 +284,9 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
         else if (var == 6 && rzWpb == 4)
             k_solve_fine<NPROL, 4, true, 4><<<cdiv(blkEnd - blk0, 4), 256, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
                                                                                  begin1, z, done, rzPart);
+        else if (var == 8)
+            k_solve_fine<NPROL, 8, true, 4><<<cdiv(blkEnd - blk0, 4), 256, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
+                                                                                 begin1, z, done, rzPart);
         else if (var == 6)
             k_solve_fine<NPROL, 4, true, 2><<<cdiv(blkEnd - blk0, 2), 128, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
                                                                                  begin1, z, done, rzPart);
@@ -304,6 +307,9 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
     } else if (var == 6) {
         k_solve_fine<NPROL, 4, false, 2><<<cdiv(blkEnd - blk0, 2), 128, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
                                                                                begin1, z, nullptr, nullptr);
+    } else if (var == 8) {  // the default form with default-policy inverse loads (fine_var)
+        k_solve_fine<NPROL, 8, false, 2><<<cdiv(blkEnd - blk0, 2), 128, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc,
+                                                                               begin1, z, nullptr, nullptr);
     } else if (var == 7) {
         k_solve_fine1c<NPROL><<<blkEnd - blk0, 64, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z);
     } else if (var == 0) {
@@ -313,6 +319,21 @@ static void launch_fine_n(int var, int g, hipStream_t s, const float4* inv, int 
         k_solve_fine<NPROL, 1, false><<<g, kApplyThreads, 0, s>>>(inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z,
                                                                     nullptr, nullptr);
     }
+}
+
+// The inverse loads' cache policy for a launch over nb level-0 blocks.  The
+// default form (6) loads them nontemporal: at 1M they are 630 MB, read once
+// per apply, more than the 256 MiB Infinity Cache keeps.  Where they and an
+// apply's vectors fit in 192 MiB (256k: 158 MB; a world-8 rank of 1M: 76 MB),
+// default-policy loads (8) let the Infinity Cache keep them from one apply to
+// the next: 256k 31.35 -> 30.51 us per apply, PCG 0.0753 -> 0.0729
+// ms/iteration; 1M 110.9 -> 125.1 us (profiles/round5/ab/fine_inv_policy/).
+// Bitwise equal.  MAS_INV_RESIDENT=0/1 forces either.
+static int fine_var(const mas_context* h, int nb) {
+    if (h->fineVariant != 6) return h->fineVariant;
+    const size_t bytes = (size_t)nb * (kBlockFloats * 4 + 32 * 48);
+    const bool resident = h->invResident >= 0 ? h->invResident != 0 : bytes <= ((size_t)192 << 20);
+    return resident ? 8 : 6;
 }
 
 // level-0 blocks [blk0, blkEnd) with prolongation of min(L,4)-1 coarse levels
@@ -325,7 +346,7 @@ void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* 
     const float4* inv = P<float4>(h->inv);
     const int4* vmap = P<int4>(h->vmap);
     const float4* zc = P<float4>(h->Zc);
-    const int begin1 = h->levelSize[3], nV = h->nV, var = h->fineVariant;
+    const int begin1 = h->levelSize[3], nV = h->nV, var = fine_var(h, blkEnd - blk0);
     const int w = h->rzWpb;
     switch (L < 4 ? L - 1 : 3) {
         case 0: launch_fine_n<0>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
@@ -337,7 +358,8 @@ void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* 
 
 // workgroups of one fine launch of the PCG's applies (= its r.z partials)
 int fine_grid(const mas_context* h) {
-    return cdiv(h->nFineBlk, h->fineVariant == 6 ? h->rzWpb : kApplyThreads / 64);
+    const int var = fine_var(h, h->nFineBlk);
+    return cdiv(h->nFineBlk, var == 6 ? h->rzWpb : var == 8 ? 4 : kApplyThreads / 64);
 }
 
 // coarse levels lFirst..L-1: level 1 from the vertices (k_coarse_l1), level
@@ -407,7 +429,7 @@ void launch_prolong(mas_context* h, int v0, int v1, float4* z, hipStream_t s) {
 void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s) {
     const int g = cdiv(blkEnd - blk0, kApplyThreads / 64);
     if (g <= 0) return;
-    launch_fine_n<0>(h->fineVariant, g, s, P<float4>(h->inv), blk0, blkEnd, h->nV, r, P<int4>(h->vmap),
+    launch_fine_n<0>(fine_var(h, blkEnd - blk0), g, s, P<float4>(h->inv), blk0, blkEnd, h->nV, r, P<int4>(h->vmap),
                      P<float4>(h->Zc), h->levelSize[3], z, nullptr, nullptr);
 }
 

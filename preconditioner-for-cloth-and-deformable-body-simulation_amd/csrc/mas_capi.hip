@@ -185,6 +185,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
         std::memset(p, 0, 64);
     }
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
+    if (const char* v = std::getenv("MAS_INV_RESIDENT")) h->invResident = std::atoi(v) != 0;
     if (const char* v = std::getenv("MAS_COARSE_OCC")) h->coarseOcc = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_NARROW")) h->coarseNarrow = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_WIDE")) h->coarseWide = std::atoi(v);

@@ -197,6 +197,7 @@ struct mas_context {
     // chunking (A/B); 3 = 1 in one-wave workgroups (A/B); 0 = default-policy
     // loads (A/B)
     int fineVariant = 6;
+    int invResident = -1;  // env MAS_INV_RESIDENT: -1 by size (fine_var, k_apply.hip), 0 / 1 forced
     // blocks (waves) per workgroup of the fine kernel in the PCG's applies,
     // one r.z partial per workgroup, summed by every SpMV workgroup (env
     // MAS_RZ_WPB: 2, 4 or 8): 4 measured 0.8-1.0 us per iteration faster

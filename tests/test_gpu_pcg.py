@@ -154,3 +154,26 @@ def test_pcg_fused_p_update_bitwise(W, L, precondition, maxit, monkeypatch):
         assert r0[k] == r1[k], (k, r0[k], r1[k])
     if maxit == 7:
         assert r1["iterations"] == 7 and not r1["converged"]
+
+
+@pytest.mark.parametrize("W,L", [(100, 3), (256, 4)])
+def test_inverse_load_policy_bitwise(W, L, monkeypatch):
+    """The fine kernel's inverse loads, nontemporal (MAS_INV_RESIDENT=0) or
+    default policy (1; chosen by size where the inverses fit the Infinity
+    Cache): the same z and the same PCG iterates bit for bit (the r.z partials
+    come from workgroups of 4 blocks either way)."""
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(W)
+    b = meshgen.residual(mesh.nV, 13)
+    out = []
+    for res_mode in ("0", "1"):
+        monkeypatch.setenv("MAS_INV_RESIDENT", res_mode)
+        P = mas_amd.from_mesh(mesh, max_levels=L)
+        z = P.Preconditioning(None, b)
+        x, res = P.pcg_solve(mesh.diag, mesh.off, mesh.starts, b, max_iters=3000, tol=TOL)
+        out.append((z, x, res))
+    (z0, x0, r0), (z1, x1, r1) = out
+    assert np.array_equal(z0.view(np.uint32), z1.view(np.uint32))
+    assert np.array_equal(x0.view(np.uint32), x1.view(np.uint32))
+    assert r0["iterations"] == r1["iterations"] and r0["true_rel_residual"] == r1["true_rel_residual"]
