@@ -280,18 +280,37 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
 // kA0 i + it (slots past s.n keep the sentinel key).  No level ids are
 // needed: a pair is a level-0 entry iff both vertices share a level-0 bank.
 constexpr int kA0 = 5;  // most vertices per stencil (EF)
-__global__ __launch_bounds__(256) void k_contact0_count(const DevStencil* __restrict__ st, int n, int* __restrict__ dCnt) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    if (i == n) {
-        dCnt[n] = 0;
-        return;
+// The early path's fills and the level-0 record counts in one launch (they
+// were five hipMemsetAsync calls and a count kernel, each a host API call on
+// the early path's critical path): add0 zeroed, the record and row keys set
+// to the sentinel (all ones) and their ids to 0, and threads i <= n count
+// stencil i's same-bank records, two per pair (n < 0: fills only).
+__global__ __launch_bounds__(256) void k_contact0_init(const DevStencil* __restrict__ st, int n, int* __restrict__ dCnt,
+                                                       float4* __restrict__ add0, size_t nAdd4,
+                                                       EntryKey* __restrict__ c0Keys, int* __restrict__ c0Ids,
+                                                       size_t ubD, unsigned* __restrict__ a0Keys,
+                                                       int* __restrict__ a0Ids, size_t ubA) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x, T = (size_t)gridDim.x * blockDim.x;
+    if (n >= 0 && i <= (size_t)n) {
+        if (i == (size_t)n) {
+            dCnt[n] = 0;
+        } else {
+            const DevStencil s = st[i];
+            int d = 0;
+            for (int x = 0; x < s.n; ++x)
+                for (int y = x + 1; y < s.n; ++y) d += ((unsigned)s.idx[x] >> 5) == ((unsigned)s.idx[y] >> 5) ? 2 : 0;
+            dCnt[i] = d;
+        }
     }
-    const DevStencil s = st[i];
-    int d = 0;
-    for (int x = 0; x < s.n; ++x)
-        for (int y = x + 1; y < s.n; ++y) d += ((unsigned)s.idx[x] >> 5) == ((unsigned)s.idx[y] >> 5) ? 2 : 0;
-    dCnt[i] = d;
+    for (size_t q = i; q < nAdd4; q += T) add0[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (size_t q = i; q < ubD; q += T) {
+        c0Keys[q] = ~(EntryKey)0;
+        c0Ids[q] = 0;
+    }
+    for (size_t q = i; q < ubA; q += T) {
+        a0Keys[q] = ~0u;
+        a0Ids[q] = 0;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_contact0_write(const DevStencil* __restrict__ st, int n,
@@ -1245,9 +1264,7 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
     if ((rc = early_buffers(h))) return rc;  // sized by run_prepare already: no allocation here
     // evPrepFork was recorded on s right after the stencils (run_prepare), before
     // the level kernels: prepStream waits for the stencils only
-    if ((rc = hip_check(h, hipStreamWaitEvent(ps, h->evPrepFork, 0), "fork wait")) ||
-        (rc = hip_check(h, hipMemsetAsync(h->add0.p, 0, (size_t)nv32 * 36, ps), "memset add0")))
-        return rc;
+    if ((rc = hip_check(h, hipStreamWaitEvent(ps, h->evPrepFork, 0), "fork wait"))) return rc;
     FineAsm fa{nV, h->maxNbr, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9, d_off9, d_ranges,
                P<float>(h->add0), nullptr, nullptr, nullptr, nullptr, nullptr};
     if (n > 0) {
@@ -1263,15 +1280,13 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
             (rc = ensure(h, h->a0Ids, ubA * 4)) || (rc = ensure(h, h->a0IdsS, ubA * 4)) ||
             (rc = ensure(h, h->a0Val, ubA * 36)) || (rc = ensure(h, h->cFineOff, (size_t)(h->nFineBlk + 1) * 4)))
             return rc;
-        // sentinel keys past the records; their ids index record 0 (never
-        // folded: a sentinel is dead, but no index is left undefined)
-        if ((rc = hip_check(h, hipMemsetAsync(h->c0Keys.p, 0xff, ubD * 4, ps), "memset keys")) ||
-            (rc = hip_check(h, hipMemsetAsync(h->a0Keys.p, 0xff, ubA * 4, ps), "memset keys")) ||
-            (rc = hip_check(h, hipMemsetAsync(h->c0Ids.p, 0, ubD * 4, ps), "memset ids")) ||
-            (rc = hip_check(h, hipMemsetAsync(h->a0Ids.p, 0, ubA * 4, ps), "memset ids")))
-            return rc;
+        // add0 zeroed, sentinel keys past the records (their ids index record
+        // 0: never folded, a sentinel is dead, but no index is left
+        // undefined), and the per-stencil counts: one launch
         const DevStencil* st = P<DevStencil>(h->stencils);
-        k_contact0_count<<<cdiv(n + 1, 256), 256, 0, ps>>>(st, n, P<int>(h->c0Cnt));
+        k_contact0_init<<<std::max(cdiv(n + 1, 256), 1024), 256, 0, ps>>>(
+            st, n, P<int>(h->c0Cnt), P<float4>(h->add0), (size_t)nv32 * 9 / 4, P<EntryKey>(h->c0Keys),
+            P<int>(h->c0Ids), ubD, P<unsigned>(h->a0Keys), P<int>(h->a0Ids), ubA);
         // prepStream's own sort / scan scratch (rs_*(..., side = true)), whatever MAS_SORT selects
         if ((rc = rs_exclusive_scan(h, P<int>(h->c0Cnt), P<int>(h->c0Off), n + 1, ps, "level-0 contact scan", true)))
             return rc;
@@ -1298,6 +1313,9 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
         fa.cids = P<int>(h->c0IdsS);
         fa.cent = P<int>(h->c0Ent);
         fa.cvals = P<float>(h->c0Val);
+    } else {  // no contacts: add0 zeroed only
+        k_contact0_init<<<1024, 256, 0, ps>>>(nullptr, -1, nullptr, P<float4>(h->add0), (size_t)nv32 * 9 / 4, nullptr,
+                                              nullptr, 0, nullptr, nullptr, 0);
     }
     // earlyOd (env MAS_EARLY_OD; default for a sharded Prepare): od and the
     // record counts need only level-0 data too and can run here, ahead of the
