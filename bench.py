@@ -32,6 +32,9 @@ region): a timing marker between the coarse launch and the fine kernel of
 every apply holds the fine kernel back several microseconds, so the per-apply
 events (apply_breakdown_ms, also reported) overstate it; the back-to-back
 average agrees with the rocprofv3 kernel trace (profiles/round5/).
+apply_breakdown_ms.coarse_back_to_back times an apply's coarse launch the
+same way (mas_profile_coarse): pre_fine, from the per-apply events, carries
+the marker delay.
 
 cpu_baseline: the CPU restatement of the reference (oracle/, OpenMP, the
 reference's packed layout and loop structure) on this host, bounded sample.
@@ -430,6 +433,9 @@ def main():
     P.set_profiling(False)
     # the roofline kernel's duration: `steps` back-to-back launches between two events
     fine_b2b_ms = P.profile_fine(z, r, args.steps, sptr) if not sharded_path else None
+    # the coarse launch(es) the same way (their per-apply events carry the marker delay too)
+    coarse_b2b_ms = (P.profile_coarse(r, args.steps, sptr)
+                     if not sharded_path and info["num_levels"] >= 2 else None)
 
     t_max = elapsed
     shard_check = None
@@ -535,6 +541,7 @@ def main():
         },
         "apply_breakdown_ms": {
             "pre_fine": round(st["pre_fine_ms_avg"], 5),
+            "coarse_back_to_back": round(coarse_b2b_ms, 5) if coarse_b2b_ms is not None else None,
             "fine_solve": round(st["fine_ms_avg"], 5),
             "post_fine": round(st["post_fine_ms_avg"], 5),
             "events_total": round(st["apply_ms_avg"], 5),

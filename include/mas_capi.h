@@ -226,6 +226,12 @@ int mas_set_profiling(mas_handle h, int enable);
  * mas_set_profiling overstate this kernel; back-to-back launches do not (the
  * roofline source of bench.py).  d_z4 is written as by an apply. */
 int mas_profile_fine(mas_handle h, float* d_z4, const float* d_r4, int n, void* stream, double* ms_per_launch);
+/* ABI 4.  The same for the coarse levels of mas_apply_device (the launch(es)
+ * before the level-0 kernel, in the form the apply uses): n back-to-back
+ * applies' coarse work, *ms_per_launch = their average.  Writes the coarse
+ * R / Z of the handle (the next apply recomputes them); z is not touched.
+ * MAS_ERR_STATE for a shard-prepared handle or at L < 2. */
+int mas_profile_coarse(mas_handle h, const float* d_r4, int n, void* stream, double* ms_per_launch);
 
 /* ---- Morton-range sharding across `world` ranks (one process per GPU) ----
  * Rank g owns a contiguous range of level-0 blocks (equal split).  Clusters

@@ -450,6 +450,18 @@ int coarse_mode(const mas_context* h) {
 // the fine waves reading tagged coarse Z -- was measured slower at every size
 // and removed: DESIGN.md section 4 "Fused apply".)
 
+// the coarse levels of an apply (run_apply), in the form it selects
+void launch_coarse_apply(mas_context* h, const float4* d_r, hipStream_t s) {
+    const int mode = coarse_mode(h);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    const bool capturing = h->L > 2 && mode == 3 &&
+                           (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone);
+    if (h->L > 2 && mode == 3 && !capturing && coarse1_supported(h))
+        launch_coarse_one(h, d_r, s);
+    else if (h->L > 2 && mode >= 2) launch_coarse_twopass(h, d_r, s);
+    else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
+}
+
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     if (h->L >= 4 && !h->deepOff.p) return fail(h, MAS_ERR_STATE, "apply: deep-level lists not built");
     if (h->fineBlk0 != 0 || h->fineBlk1 != h->nFineBlk)
@@ -461,14 +473,7 @@ int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s) {
     // coarse levels (mas_internal.h coarseMode); every form bitwise equal.  The
     // one-launch form's tags carry a host-side epoch, which a graph capture
     // would freeze: a capturing stream gets the two-launch form.
-    const int mode = coarse_mode(h);
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    const bool capturing = h->L > 2 && mode == 3 &&
-                           (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone);
-    if (h->L > 2 && mode == 3 && !capturing && coarse1_supported(h))
-        launch_coarse_one(h, d_r, s);
-    else if (h->L > 2 && mode >= 2) launch_coarse_twopass(h, d_r, s);
-    else if (h->L > 1) launch_coarse_levels(h, 1, d_r, s);
+    launch_coarse_apply(h, d_r, s);
     if (ev) hipEventRecord(ev[1], s);
     launch_fine(h, 0, h->nFineBlk, d_r, d_z, s, h->applyDone, h->applyRzPart);
     if (ev) hipEventRecord(ev[2], s);

@@ -428,6 +428,29 @@ int mas_profile_fine(mas_handle h, float* d_z4, const float* d_r4, int n, void* 
     return MAS_OK;
 }
 
+int mas_profile_coarse(mas_handle h, const float* d_r4, int n, void* stream, double* ms_per_launch) {
+    if (!h) return MAS_ERR_ARG;
+    if (!d_r4 || !ms_per_launch || n <= 0) return fail(h, MAS_ERR_ARG, "mas_profile_coarse: bad arguments");
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "profile before prepare");
+    if (h->fineBlk0 != 0 || h->fineBlk1 != h->nFineBlk)
+        return fail(h, MAS_ERR_STATE, "mas_profile_coarse: the handle was prepared for one shard");
+    if (h->L < 2) return fail(h, MAS_ERR_STATE, "mas_profile_coarse: no coarse level");
+    MAS_TRY(pending_giveup(h));
+    hipSetDevice(h->device);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    ScopedEvents ev;
+    if (!ev.ok()) return fail(h, MAS_ERR_HIP, "hipEventCreate");
+    MAS_TRY(hip_check(h, hipEventRecord(ev.e[0], s), "record"));
+    for (int i = 0; i < n; ++i) launch_coarse_apply(h, reinterpret_cast<const float4*>(d_r4), s);
+    MAS_TRY(hip_check(h, hipGetLastError(), "coarse kernels"));
+    MAS_TRY(hip_check(h, hipEventRecord(ev.e[1], s), "record"));
+    MAS_TRY(hip_check(h, hipEventSynchronize(ev.e[1]), "profile sync"));
+    float ms = 0.f;
+    MAS_TRY(hip_check(h, hipEventElapsedTime(&ms, ev.e[0], ev.e[1]), "elapsed"));
+    *ms_per_launch = (double)ms / n;
+    return pending_giveup(h);
+}
+
 int mas_get_info(mas_handle h, mas_info* out) {
     if (!h || !out) return MAS_ERR_ARG;
     std::memset(out, 0, sizeof(*out));

@@ -457,6 +457,7 @@ int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const in
 // level-0 blocks [blk0, blkEnd) + prolongation; done / rzPart: PCG hooks (k_apply.hip)
 void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s,
                  const int* done = nullptr, double* rzPart = nullptr);
+void launch_coarse_apply(mas_context* h, const float4* d_r, hipStream_t s);  // the coarse levels of run_apply
 void launch_fine_z0(mas_context* h, int blk0, int blkEnd, const float4* r, float4* z, hipStream_t s);
 void launch_prolong(mas_context* h, int v0, int v1, float4* z, hipStream_t s);
 int fine_grid(const mas_context* h);  // workgroups of one fine launch over every level-0 block

@@ -36,7 +36,8 @@ ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 
 # every entry point declared in include/mas_capi.h
 EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_allocate", "mas_prepare",
-           "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_profile_fine", "mas_get_info",
+           "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_profile_fine",
+           "mas_profile_coarse", "mas_get_info",
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
            "mas_get_coarse_residual", "mas_set_prepare_shard",
            "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
@@ -128,6 +129,7 @@ def lib():
         L.mas_apply_device.argtypes = [P, P, P, P]
         L.mas_set_profiling.argtypes = [P, I]
         L.mas_profile_fine.argtypes = [P, P, P, I, P, ctypes.POINTER(ctypes.c_double)]
+        L.mas_profile_coarse.argtypes = [P, P, I, P, ctypes.POINTER(ctypes.c_double)]
         L.mas_get_info.argtypes = [P, ctypes.POINTER(mas_info)]
         L.mas_get_stats.argtypes = [P, ctypes.POINTER(mas_stats)]
         L.mas_get_maps.argtypes = [P, P, P, P, P, P, P, P]
@@ -464,6 +466,15 @@ class SeSchwarzPreconditioner:
         out = ctypes.c_double()
         self._check(self._L.mas_profile_fine(self.h, _ptr(z), _ptr(r), int(n), _ptr(stream), ctypes.byref(out)),
                     "profile_fine")
+        return out.value
+
+    def profile_coarse(self, r, n, stream=None) -> float:
+        """Average ms of an apply's coarse launch(es) alone over n back-to-back applies' worth (mas_profile_coarse)."""
+        self._need("profile_coarse")
+        r = _dev(r, self._nV, 4, "float32", "r")
+        out = ctypes.c_double()
+        self._check(self._L.mas_profile_coarse(self.h, _ptr(r), int(n), _ptr(stream), ctypes.byref(out)),
+                    "profile_coarse")
         return out.value
 
     def info(self) -> dict:

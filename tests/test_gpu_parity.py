@@ -420,3 +420,23 @@ def test_profile_fine_writes_the_apply_z():
     s.synchronize()
     assert ms > 0
     assert torch.equal(z1, z2)
+
+
+@pytest.mark.parametrize("L", [2, 3, 4])
+def test_profile_coarse_leaves_the_apply_unchanged(L):
+    """mas_profile_coarse (bench.py's coarse_back_to_back) launches the apply's
+    own coarse form: the coarse R / Z it rewrites are the ones the next apply
+    recomputes, so z after it is bitwise the apply's; the duration is positive."""
+    import torch
+    from mas_amd import meshgen
+    mesh = cloth(256)
+    P = _gpu(mesh, L, reference_formation=False)
+    r = torch.from_numpy(meshgen.residual(mesh.nV, 5)).cuda()
+    z1, z2 = torch.zeros_like(r), torch.zeros_like(r)
+    s = torch.cuda.Stream()
+    P.PreconditioningDevice(z1, r, s.cuda_stream)
+    ms = P.profile_coarse(r, 5, s.cuda_stream)
+    P.PreconditioningDevice(z2, r, s.cuda_stream)
+    s.synchronize()
+    assert ms > 0
+    assert torch.equal(z1, z2)
