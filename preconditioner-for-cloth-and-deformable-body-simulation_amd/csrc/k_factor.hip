@@ -121,26 +121,30 @@ __device__ __forceinline__ float quad_bcast(float x, int sel) {
 }
 
 template <int X>
-__device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float* dinv, int rg, int cg) {
+__device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float (&dv)[2], int rg, int cg) {
     constexpr int mX = X / 16, rX = X % 16, cgX = X / 24, cX = X % 24;
     constexpr int mLo = (X < 15) ? 0 : (X - 15) / 16 + 1;
     float* pr = piv;  // one buffer: a single wave's LDS operations complete in order
+    // The pivot straight from its owner lane (lane 4 rX + cgX holds A[X][X] in
+    // v[mX][cX]; the same value the pivot row carries through LDS), so the
+    // step's three IEEE divisions -- D^-1_X and the quotients of two rows per
+    // lane -- start at once, unconditionally and side by side, while the
+    // pivot row makes its LDS round trip.  (Read from LDS after the row's
+    // store, each division in the branch of its lanes, they ran one after the
+    // other behind that round trip.)
+    const float pd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[mX][cX]), 4 * rX + cgX));
     if (rg == rX) {
 #pragma unroll
         for (int c4 = 0; c4 < 6; ++c4)
             *reinterpret_cast<float4*>(&pr[24 * cg + 4 * c4]) =
                 make_float4(v[mX][4 * c4], v[mX][4 * c4 + 1], v[mX][4 * c4 + 2], v[mX][4 * c4 + 3]);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // the pivot is final from this step on: D^-1_X (.cpp:1429-1433) here, by
-    // every lane (no divergent branch; measured 1.75 vs 1.86 ms at 1M with the
-    // division in the pivot lane's branch)
-    const float pd = pr[X];
+    // every lane; lane X % 64 keeps it (dv[X / 64], a select, no branch) and
+    // stores it after the elimination
     {
         const float d = __fdiv_rn(1.0f, pd);
-        if (rg == 0 && cg == 0) dinv[X] = d;
+        dv[X / 64] = (4 * rg + cg == X % 64) ? d : dv[X / 64];
     }
     if constexpr (mLo <= 5) {
         float a[6], r[6];
@@ -160,11 +164,16 @@ __device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float* di
             const bool act1 = m1 < 6 && rg + 16 * m1 > X && a1 != 0.0f;
             // (a shared-reciprocal division without the scale / fixup steps,
             // exact for operands in [2^-40, 2^40], measured 11 % slower)
-            if (act0) q0 = __fdiv_rn(-a0, pd);
-            if (act1) q1 = __fdiv_rn(-a1, pd);
+            const float d0 = __fdiv_rn(-a0, pd), d1 = __fdiv_rn(-a1, pd);  // every lane, then selected
+            q0 = act0 ? d0 : 0.f;
+            q1 = act1 ? d1 : 0.f;
         }
 #pragma unroll
         for (int m = mLo; m < 6; ++m) r[m] = quad_bcast((m - mLo) < 4 ? q0 : q1, (m - mLo) & 3);
+        // the pivot row's LDS store before its loads below
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         // the pivot row in two halves of 12 (register budget: 2 waves per SIMD)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
@@ -216,14 +225,14 @@ __device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float* di
 
 template <int X>
 struct ElimRB {
-    static __device__ __forceinline__ void run(float (&v)[6][24], float* piv, float* dinv, int rg, int cg) {
-        rb_step<X>(v, piv, dinv, rg, cg);
-        ElimRB<X + 1>::run(v, piv, dinv, rg, cg);
+    static __device__ __forceinline__ void run(float (&v)[6][24], float* piv, float (&dv)[2], int rg, int cg) {
+        rb_step<X>(v, piv, dv, rg, cg);
+        ElimRB<X + 1>::run(v, piv, dv, rg, cg);
     }
 };
 template <>
 struct ElimRB<96> {
-    static __device__ __forceinline__ void run(float (&)[6][24], float*, float*, int, int) {}
+    static __device__ __forceinline__ void run(float (&)[6][24], float*, float (&)[2], int, int) {}
 };
 
 // Zero diagonal -> identity node block (.cpp:1365-1368), applied in place to
@@ -392,7 +401,10 @@ __device__ __forceinline__ void factor_tiles(float (&v)[6][24], float* M, float*
                                              const uint4* __restrict__ tileSlot, const uint4* __restrict__ valuSlot,
                                              int t, int* status, int blk) {
     const int rg = t >> 2, cg = t & 3;
-    ElimRB<0>::run(v, piv, dinv, rg, cg);
+    float dv[2] = {0.f, 0.f};  // D^-1 of steps t and 64 + t
+    ElimRB<0>::run(v, piv, dv, rg, cg);
+    dinv[t] = dv[0];
+    if (t < 32) dinv[64 + t] = dv[1];
     // M rows: unit diagonal, L^-1 below, only the stored (padded) columns
 #pragma unroll
     for (int m = 0; m < 6; ++m) {
