@@ -139,10 +139,10 @@ __device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float (&d
             *reinterpret_cast<float4*>(&pr[24 * cg + 4 * c4]) =
                 make_float4(v[mX][4 * c4], v[mX][4 * c4 + 1], v[mX][4 * c4 + 2], v[mX][4 * c4 + 3]);
     }
-    // the pivot is final from this step on: D^-1_X (.cpp:1429-1433) here, by
-    // every lane; lane X % 64 keeps it (dv[X / 64], a select, no branch) and
-    // stores it after the elimination
-    {
+    // the pivot is final from this step on: D^-1_X (.cpp:1429-1433) is taken
+    // here; lane X % 64 keeps it (dv[X / 64], a select, no branch) and stores
+    // it after the elimination
+    if constexpr (mLo > 5) {
         const float d = __fdiv_rn(1.0f, pd);
         dv[X / 64] = (4 * rg + cg == X % 64) ? d : dv[X / 64];
     }
@@ -164,9 +164,15 @@ __device__ __forceinline__ void rb_step(float (&v)[6][24], float* piv, float (&d
             const bool act1 = m1 < 6 && rg + 16 * m1 > X && a1 != 0.0f;
             // (a shared-reciprocal division without the scale / fixup steps,
             // exact for operands in [2^-40, 2^40], measured 11 % slower)
-            const float d0 = __fdiv_rn(-a0, pd), d1 = __fdiv_rn(-a1, pd);  // every lane, then selected
+            // every lane divides twice, then selects.  A cg == 3 lane never owns
+            // row group m1 = mLo + 7 > 5, so its second division is -1 / pd
+            // instead, and D^-1_X = -(-1 / pd) (IEEE division is symmetric in
+            // sign): two division sequences per step instead of three
+            const float d0 = __fdiv_rn(-a0, pd), d1 = __fdiv_rn(cg == 3 ? -1.0f : -a1, pd);
             q0 = act0 ? d0 : 0.f;
             q1 = act1 ? d1 : 0.f;
+            const float d = -__int_as_float(__builtin_amdgcn_readlane(__float_as_int(d1), 3));
+            dv[X / 64] = (4 * rg + cg == X % 64) ? d : dv[X / 64];
         }
 #pragma unroll
         for (int m = mLo; m < 6; ++m) r[m] = quad_bcast((m - mLo) < 4 ? q0 : q1, (m - mLo) & 3);
