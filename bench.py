@@ -224,17 +224,38 @@ def run_launcher(cmd):
     """Run the ranks as ONE child process tree (never an exec: nothing in this
     process has touched the GPU, and nothing will); rank 0's JSON line goes to
     stdout, every other line of the children's stdout to stderr."""
+    import signal
     import subprocess
     log("bench.py: launching " + " ".join(cmd[1:]))
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
-    for line in p.stdout:
-        s = line.strip()
-        if s.startswith("{") and '"metric"' in s:
-            print(s, flush=True)
-        else:
-            sys.stderr.write(line)
-            sys.stderr.flush()
-    return p.wait()
+
+    def die_with_parent():
+        # the launcher (and through it every rank) gets SIGTERM if this
+        # process dies first, e.g. killed by a driver's time limit: no rank is
+        # left holding a GPU
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1, preexec_fn=die_with_parent)
+
+    def forward(signum, _frame):  # SIGTERM / SIGINT to this process: pass it on, then wait for the ranks
+        p.send_signal(signum)
+
+    old = {sig: signal.signal(sig, forward) for sig in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for line in p.stdout:
+            s = line.strip()
+            if s.startswith("{") and '"metric"' in s:
+                print(s, flush=True)
+            else:
+                sys.stderr.write(line)
+                sys.stderr.flush()
+        return p.wait()
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
 
 
 def check_rank_layout(gpus, world, local, ndev, backend):
@@ -264,6 +285,8 @@ def launch_check(args, rank, world, local):
         print(json.dumps({"metric": "launch-check", **out}), flush=True)
     else:
         print(json.dumps(out), flush=True)
+    # tests/test_bench_launch.py: ranks that stay up until the parent is stopped
+    time.sleep(float(os.environ.get("BENCH_LAUNCH_CHECK_SLEEP", "0")))
 
 
 def main():

@@ -58,3 +58,43 @@ def test_plain_bench_launches_n_ranks(backend):
 def test_launcher_world_mismatch_fails():
     p = _run(["--gpus", "3", "--launch-check"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
     assert p.returncode == 2 and "WORLD_SIZE=2" in p.stderr
+
+
+def test_launcher_ranks_end_with_the_parent():
+    """A parent bench.py that is terminated takes its launcher and every rank
+    with it (signal forwarding + PR_SET_PDEATHSIG): nothing is left holding a
+    GPU after a driver's time limit."""
+    import signal
+    import threading
+    import time
+    import psutil
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_LAUNCH_CHECK_SLEEP="120")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--launch-check",
+                          "--dist-backend", "gloo"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         env=env, cwd=REPO, start_new_session=True)
+    err = []
+    threading.Thread(target=lambda: err.extend(p.stderr), daemon=True).start()
+    try:
+        deadline = time.time() + 150
+        while time.time() < deadline and not any('"rank": 1' in l for l in err):
+            time.sleep(0.5)
+        assert any('"rank": 1' in l for l in err), "".join(err)[-2000:]
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) != 0
+        time.sleep(2)
+        left = [q.pid for q in psutil.process_iter() if _sid(q.pid) == p.pid and q.pid != p.pid]
+        assert not left, left
+    finally:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+
+
+def _sid(pid):
+    try:
+        return os.getsid(pid)
+    except OSError:
+        return None
