@@ -81,20 +81,19 @@ def test_launcher_ranks_end_with_the_parent():
         while time.time() < deadline and not any('"rank": 1' in l for l in err):
             time.sleep(0.5)
         assert any('"rank": 1' in l for l in err), "".join(err)[-2000:]
+        tree = psutil.Process(p.pid).children(recursive=True)  # the launcher and its ranks (own sessions)
+        assert len(tree) >= 3, tree
         p.send_signal(signal.SIGTERM)
         assert p.wait(timeout=60) != 0
-        time.sleep(2)
-        left = [q.pid for q in psutil.process_iter() if _sid(q.pid) == p.pid and q.pid != p.pid]
-        assert not left, left
+        gone, alive = psutil.wait_procs(tree, timeout=30)
+        assert not alive, [q.pid for q in alive]
     finally:
+        for q in locals().get("tree", []):
+            try:
+                q.kill()
+            except psutil.Error:
+                pass
         try:
             os.killpg(p.pid, signal.SIGKILL)
         except OSError:
             pass
-
-
-def _sid(pid):
-    try:
-        return os.getsid(pid)
-    except OSError:
-        return None
