@@ -349,12 +349,31 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ float m_at(const float* M, int k, int i) {
     return i < k ? M[m_row(k) + i] : (i == k ? 1.f : 0.f);
 }
-__device__ __forceinline__ v16f mfma_tile(const float* M, const float* dinv, int I, int J, int col, int kh) {
+// Tile (I, J), fully unrolled and branch-free: row k of M starts at the
+// uniform m_row(k) (a select between the two rows of a k pair by the lane's
+// half), columns past k read the row's stored unit diagonal (clamped address)
+// and are zeroed by a select -- the same operands as m_at, so the same bits.
+// (The first form evaluated m_at per operand with branches and a runtime k
+// loop: ~30 instructions and an LDS wait per MFMA, 0.57 ms of the 2.10 ms
+// fused kernel at 1M + contacts.)
+template <int I, int J>
+__device__ __forceinline__ v16f mfma_tile(const float* M, const float* dinv, int col, int kh) {
     v16f acc = {};
+    const int ci = 32 * I + col, cj = 32 * J + col;
+#pragma unroll
     for (int k0 = 94; k0 >= 32 * J; k0 -= 2) {
         const int k = k0 + 1 - kh;  // the instruction is the fmaf chain k-half 0 then 1: strictly k-descending
-        const float a = m_at(M, k, 32 * I + col);
-        const float b = __fmul_rn(dinv[k], m_at(M, k, 32 * J + col));
+        const int rb = kh ? m_row(k0) : m_row(k0 + 1);
+        float a;
+        if constexpr (I < J) {
+            a = M[rb + ci];  // ci < 32 J <= k: strictly below the diagonal
+        } else {
+            a = M[rb + min(ci, k)];
+            a = ci <= k ? a : 0.f;
+        }
+        float m = M[rb + min(cj, k)];
+        m = cj <= k ? m : 0.f;
+        const float b = __fmul_rn(dinv[k], m);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
     }
     return acc;
@@ -374,12 +393,12 @@ __device__ __forceinline__ void form_mfma(float* M, const float* dinv, float* ou
 #pragma unroll
     for (int q = 0; q < 12; ++q) sl[q] = tileSlot[q * 64 + lane];
     v16f acc[6];
-    acc[0] = mfma_tile(M, dinv, 0, 0, col, kh);
-    acc[1] = mfma_tile(M, dinv, 0, 1, col, kh);
-    acc[2] = mfma_tile(M, dinv, 1, 1, col, kh);
-    acc[3] = mfma_tile(M, dinv, 0, 2, col, kh);
-    acc[4] = mfma_tile(M, dinv, 1, 2, col, kh);
-    acc[5] = mfma_tile(M, dinv, 2, 2, col, kh);
+    acc[0] = mfma_tile<0, 0>(M, dinv, col, kh);
+    acc[1] = mfma_tile<0, 1>(M, dinv, col, kh);
+    acc[2] = mfma_tile<1, 1>(M, dinv, col, kh);
+    acc[3] = mfma_tile<0, 2>(M, dinv, col, kh);
+    acc[4] = mfma_tile<1, 2>(M, dinv, col, kh);
+    acc[5] = mfma_tile<2, 2>(M, dinv, col, kh);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every M read done before M is overwritten
     __builtin_amdgcn_wave_barrier();
     float* O = M;  // 4 656 <= kPackedM floats
@@ -408,7 +427,11 @@ __device__ __forceinline__ void factor_tiles(float (&v)[6][24], float* M, float*
                                              int t, int* status, int blk) {
     const int rg = t >> 2, cg = t & 3;
     float dv[2] = {0.f, 0.f};  // D^-1 of steps t and 64 + t
+#ifndef MAS_TIMING_NO_ELIM  // timing probe only (A/B build): the kernel without its elimination
     ElimRB<0>::run(v, piv, dv, rg, cg);
+#else
+    dv[0] = dv[1] = 1.f;
+#endif
     dinv[t] = dv[0];
     if (t < 32) dinv[64 + t] = dv[1];
     // M rows: unit diagonal, L^-1 below, only the stored (padded) columns
@@ -433,6 +456,10 @@ __device__ __forceinline__ void factor_tiles(float (&v)[6][24], float* M, float*
     }
     __syncthreads();
     if (status) check_pivots(dinv, status, blk, t);
+#ifdef MAS_TIMING_NO_FORM  // timing probe only (A/B build): no inverse formation
+    if (t == 0) out[0] = M[0] + dinv[0];
+    return;
+#endif
     if (MFMA) form_mfma(M, dinv, out, tileSlot, t);  // one wave: no barrier around M
     else form_packed_staged(M, dinv, out, valuSlot, t);
 }
