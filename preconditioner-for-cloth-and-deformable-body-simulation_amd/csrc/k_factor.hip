@@ -638,6 +638,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const int t = threadIdx.x;
     const int blk = blk0 + blockIdx.x;
     float v[6][24];
+#ifndef MAS_TIMING_NO_ASM  // timing probe only (A/B build): the kernel without its assembly
     build_slab<0>(a, blk, M, t);
     slab_to_tiles<0>(v, M, t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab 0 read before slab 1 overwrites it
@@ -646,6 +647,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     slab_to_tiles<1>(v, M, t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
+#else
+    for (int m = 0; m < 6; ++m)
+        for (int c = 0; c < 24; ++c) v[m][c] = (t >> 2) + 16 * m == 24 * (t & 3) + c ? 2.f : 0.01f * (float)(c + m);
+#endif
     factor_tiles<MFMA>(v, M, piv, dinv, inv + (size_t)blk * kBlockFloats, tileSlot, valuSlot, t, status, blk);
 }
 
