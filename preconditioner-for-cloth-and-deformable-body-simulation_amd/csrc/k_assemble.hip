@@ -573,13 +573,26 @@ __global__ __launch_bounds__(256) void k_od_lanes(FineAsm a, float* __restrict__
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int v = t / G, j = t % G, g0 = lane & ~(G - 1);
     const bool vin = v < a.nV;
-    int o = 0, num = 0;
-    if (vin) {
-        o = a.s2o[v];
-        num = a.nbrNum[v];
-    }
+    const int vc = vin ? v : 0;
+    // every load issued as early as its address allows: the s2o -> ranges ->
+    // off9 chain, and beside it nbr, the vertex's diagonal (after s2o) and
+    // additional rows, which the folding lanes need after the barrier (a
+    // fourth dependent round trip when they were loaded there; beside the
+    // fused kernel this kernel runs on the reserved CUs and is bound by those
+    // round trips)
+    const int o = vin ? a.s2o[v] : 0;
+    const int num = vin ? a.nbrNum[v] : 0;
     const int k = 1 + j;
     const unsigned ot = vin && k < num ? (unsigned)a.nbr[(size_t)k * a.nV + v] : 0xffffffffu;
+    // lane j folds entries j (and j + G when G = 8: lane 0 also folds entry 8)
+    float dd[2], aa[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int q = j + G * i, r = q / 3, c = q % 3;
+        const bool fold = q < 9;
+        dd[i] = fold ? a.diag9[9 * (size_t)o + c * 3 + r] : 0.f;
+        aa[i] = fold ? a.additional[9 * (size_t)vc + r * 3 + c] : 0.f;
+    }
     const bool has = vin && k < num;
     const bool same = has && (ot >> 5) == ((unsigned)v >> 5);
     const unsigned long long bs = __ballot(has && !same);
@@ -600,12 +613,11 @@ __global__ __launch_bounds__(256) void k_od_lanes(FineAsm a, float* __restrict__
     stg[w][lane][9] = same ? 1.f : 0.f;
     __syncthreads();
     if (!vin) return;
-    // lane j folds entries j (and 8 when G = 8, lane 0) of the vertex's od
-    for (int q = j; q < 9; q += G) {
-        const int r = q / 3, c = q % 3;
-        const float* d = a.diag9 + 9 * (size_t)o;
-        const float* ad = a.additional + 9 * (size_t)v;
-        float acc = __fadd_rn(d[c * 3 + r], ad[r * 3 + c]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int q = j + G * i;
+        if (q >= 9) break;
+        float acc = __fadd_rn(dd[i], aa[i]);
         for (int s = 0; s < G && 1 + s < num; ++s)
             if (stg[w][g0 + s][9] != 0.f) acc = __fadd_rn(acc, stg[w][g0 + s][q]);
         od[9 * (size_t)v + q] = acc;
@@ -821,8 +833,13 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __
 // bank's vertices mostly share one level-1 node, so the running entry stays in
 // registers and is written back only when the parent changes (the same left
 // fold, without a dependent read-modify-write of HBM per vertex).
+// The bank's parents and od rows are loaded 8 vertices at a time, all loads
+// of a batch issued before its adds (one dependent round trip per batch
+// instead of one per vertex: beside the fused kernel this kernel runs on the
+// reserved CUs and was bound by those round trips).
 __global__ __launch_bounds__(256) void k_diag1(int nV, const int* __restrict__ gn, const float* __restrict__ od,
                                                float* __restrict__ dense) {
+    constexpr int kB = 8;
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w * 32 >= nV) return;
     const int end = min(w * 32 + 32, nV);
@@ -830,19 +847,32 @@ __global__ __launch_bounds__(256) void k_diag1(int nV, const int* __restrict__ g
     float acc[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) acc[r * 3 + c] = entry(dense, cur, cur)[r * 96 + c];
-    for (int u = w * 32; u < end; ++u) {
-        const unsigned p = (unsigned)gn[u];
-        if (p != cur) {
-            float* e = entry(dense, cur, cur);
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
-            cur = p;
-            e = entry(dense, cur, cur);
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
+    for (int u0 = w * 32; u0 < end; u0 += kB) {
+        unsigned pb[kB];
+        float ob[kB][9];
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+            const int u = min(u0 + i, end - 1);  // clamped: the tail's extra rows are not added
+            pb[i] = (unsigned)gn[u];
+            const float* a = od + 9 * (size_t)u;
+#pragma unroll
+            for (int e = 0; e < 9; ++e) ob[i][e] = a[e];
         }
-        const float* a = od + 9 * (size_t)u;
-        for (int e = 0; e < 9; ++e) acc[e] = __fadd_rn(acc[e], a[e]);
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+            if (u0 + i >= end) break;
+            if (pb[i] != cur) {
+                float* e = entry(dense, cur, cur);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) e[r * 96 + c] = acc[r * 3 + c];
+                cur = pb[i];
+                e = entry(dense, cur, cur);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) acc[r * 3 + c] = e[r * 96 + c];
+            }
+#pragma unroll
+            for (int e = 0; e < 9; ++e) acc[e] = __fadd_rn(acc[e], ob[i][e]);
+        }
     }
     float* e = entry(dense, cur, cur);
     for (int r = 0; r < 3; ++r)
