@@ -559,6 +559,13 @@ __device__ __forceinline__ void build_slab(const FineAsm& a, int blk, float* S, 
         num = a.nbrNum[v];
         base = a.ranges[o];
     }
+    // Column masks per node (past the staging area): a slab whose slots never
+    // name one (node, column) entry twice -- no duplicate neighbour, no self
+    // loop, the usual case -- gives every entry at most one CSR term, so all
+    // slots' adds can go at once; otherwise they go in slot order (below).
+    unsigned* colMask = reinterpret_cast<unsigned*>(S + 48 * 96 + 16 * 10);
+    if (lane < 16) colMask[lane] = 0u;
+    __syncthreads();
     for (int k0 = 0; k0 < a.maxNbr; k0 += 16) {
         float m[4][9];
         int col[4];
@@ -586,17 +593,33 @@ __device__ __forceinline__ void build_slab(const FineAsm& a, int blk, float* S, 
                 col[p] = (int)(ot & 31);
             }
         }
+        bool dup = false;
 #pragma unroll
         for (int p = 0; p < 4; ++p)
+            if (col[p] >= 0) dup |= (atomicOr(&colMask[n], 1u << col[p]) >> col[p]) & 1u;
+        if (!__ballot(dup)) {  // every entry of this pass gets one term: all adds at once
 #pragma unroll
-            for (int gg = 0; gg < 4; ++gg)  // slot order within the vertex (duplicate neighbours add in ELL order)
-                if (g == gg && col[p] >= 0) {
+            for (int p = 0; p < 4; ++p)
+                if (col[p] >= 0) {
                     float* e = S + (3 * n) * 96 + 3 * col[p];
 #pragma unroll
                     for (int r = 0; r < 3; ++r)
 #pragma unroll
                         for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], m[p][r * 3 + c]);
                 }
+        } else {
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int gg = 0; gg < 4; ++gg)  // slot order within the vertex (duplicate neighbours add in ELL order)
+                    if (g == gg && col[p] >= 0) {
+                        float* e = S + (3 * n) * 96 + 3 * col[p];
+#pragma unroll
+                        for (int r = 0; r < 3; ++r)
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) e[r * 96 + c] = __fadd_rn(e[r * 96 + c], m[p][r * 3 + c]);
+                    }
+        }
     }
     __syncthreads();
     if (lane < 16) {  // zero diagonal -> identity node block (.cpp:1365-1368)
@@ -631,7 +654,7 @@ template <bool MFMA>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_fused(
     FineAsm a, float* __restrict__ inv, const uint4* __restrict__ tileSlot, const uint4* __restrict__ valuSlot,
     int blk0, int* __restrict__ status) {
-    static_assert(48 * 96 + 16 * 10 <= kPackedM, "a slab and 16 staged contact records fit in M's LDS");
+    static_assert(48 * 96 + 16 * 10 + 16 <= kPackedM, "a slab, 16 staged contact records and 16 column masks fit in M's LDS");
     __shared__ __attribute__((aligned(16))) float M[kPackedM];
     __shared__ __attribute__((aligned(16))) float piv[96];
     __shared__ float dinv[96];

@@ -440,3 +440,48 @@ def test_profile_coarse_leaves_the_apply_unchanged(L):
     s.synchronize()
     assert ms > 0
     assert torch.equal(z1, z2)
+
+
+def _with_duplicate_neighbours(mesh, pairs):
+    """A copy of mesh whose CSR names each (v, u) of pairs twice (and (u, v)),
+    the second copy with its own off-diagonal block (0.5 of the first, its
+    share added to both diagonals): a
+    duplicate neighbour, legal input for the reference (.cpp:1257-1343 adds
+    every CSR entry in slot order)."""
+    import copy
+    starts, idx, off = mesh.starts.astype(np.int64), mesh.idx.copy(), mesh.off.copy()
+    rows = [list(zip(idx[starts[v]:starts[v + 1]].tolist(), off[starts[v]:starts[v + 1]])) for v in range(mesh.nV)]
+    diag = mesh.diag.copy()
+    for v, u in pairs:
+        for a, b in ((v, u), (u, v)):
+            k = [t[0] for t in rows[a]].index(b)
+            blk = (0.5 * rows[a][k][1]).astype(np.float32)
+            rows[a].insert(k + 1, (b, blk))
+            diag[a] -= blk  # the spring's diagonal share, so the Hessian stays SPD
+    m = copy.copy(mesh)
+    m.diag = diag
+    m.starts = np.zeros(mesh.nV + 1, np.int32)
+    m.starts[1:] = np.cumsum([len(r) for r in rows])
+    m.idx = np.array([t[0] for r in rows for t in r], np.int32)
+    m.off = np.ascontiguousarray(np.array([t[1] for r in rows for t in r], np.float32))
+    return m
+
+
+def test_duplicate_neighbours_bitwise():
+    """Duplicate neighbours take the slab assembly's slot-ordered path (a
+    pass whose slots name one entry twice); every other pass adds all slots
+    at once.  Level-0 blocks and inverses stay bitwise the oracle's either way."""
+    from mas_amd import meshgen
+    base = cloth(40)
+    mesh = _with_duplicate_neighbours(base, [(0, 1), (100, 141), (777, 778)])
+    assert mesh.nnz == base.nnz + 6
+    P = _gpu(mesh, 2, keep_blocks=True)
+    o = _oracle(mesh, 2)
+    compare_maps(P, o, mesh.nV)
+    nfine = (mesh.nV + 31) // 32
+    o2s = P.maps()["o2s"]
+    for blk in sorted({int(o2s[v]) // 32 for v in (0, 1, 100, 141, 777, 778)} | {0, nfine - 1}):
+        np.testing.assert_array_equal(P.block_matrix(blk), o.block_matrix(blk))
+        np.testing.assert_array_equal(P.block_inverse(blk), o.block_inverse(blk))
+    r = meshgen.residual(mesh.nV, 21)
+    assert rel_err(P.Preconditioning(None, r), o.apply(r)) <= Z_TOL
