@@ -1434,6 +1434,35 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                h->cfg.keep_blocks ? dense : nullptr};
     bool forked = false;
     if (h->nStencil && (rc = run_contacts(h, s, fc, fa, forked))) return rc;
+    // With the records cached, their fold (off-diagonal coarse entries only:
+    // a record's nodes differ at its level) needs nothing od, k_diag1 or the
+    // table folds (diagonal entries) produce: it can run on a side stream
+    // beside them, after the contacts' records (added first, as the
+    // reference), joining before the coarse factor.  A sharded Prepare, whose
+    // critical path is this chain: world-8 rank at 1M + contacts 1.33-1.36 ->
+    // 1.28-1.29 ms; unsharded, where the fused level-0 kernel is as long, the
+    // side fold slows that kernel (1.83 -> 1.90 ms) and Prepare 2.35-2.37 ->
+    // 2.36-2.41 (profiles/round5/ab/fold_side/), so it stays in line there.
+    const bool sideWanted = h->foldSide > 0 || (h->foldSide < 0 && h->prepWorld > 1);
+    const bool sideFold = L > 1 && sideWanted && h->hierCache && h->recHierId == h->hierId && !h->rangesChanged &&
+                          h->nRecCached > 0;
+    if (sideFold) {
+        if (!h->foldStream && ((rc = hip_check(h, hipStreamCreateWithFlags(&h->foldStream, hipStreamNonBlocking),
+                                               "fold stream")) ||
+                               (rc = hip_check(h, hipEventCreateWithFlags(&h->evFoldFork, hipEventDisableTiming),
+                                               "fold event")) ||
+                               (rc = hip_check(h, hipEventCreateWithFlags(&h->evFoldJoin, hipEventDisableTiming),
+                                               "fold event"))))
+            return rc;
+        const RecKey rk0{h->levelSize[3], bit_width((unsigned)(tc - h->levelSize[3]))};
+        if ((rc = hip_check(h, hipEventRecord(h->evFoldFork, s), "fold fork")) ||
+            (rc = hip_check(h, hipStreamWaitEvent(h->foldStream, h->evFoldFork, 0), "fold fork wait")))
+            return rc;
+        k_fold_runs<DenseEntry, true, EntryKey><<<cdiv(h->nRecCached, 64), 64, 0, h->foldStream>>>(
+            h->nRecCached, rk0.dead(), P<EntryKey>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
+            DenseEntry{dense, rk0});
+        if ((rc = hip_check(h, hipEventRecord(h->evFoldJoin, h->foldStream), "fold join"))) return rc;
+    }
     if (fused) {
         // the level-0 blocks assemble and factor on prepStream while this
         // stream assembles the coarse levels (run_factor joins); the early
@@ -1469,7 +1498,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     if (valence > 64) return fail(h, MAS_ERR_ARG, "more than 64 neighbours per vertex");
     if (cached) {
         const int nRec = h->nRecCached;
-        if (nRec > 0)
+        if (nRec > 0 && !sideFold)
             k_fold_runs<DenseEntry, true, EntryKey><<<cdiv(nRec, 64), 64, 0, s>>>(
                 nRec, rk.dead(), P<EntryKey>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
                 DenseEntry{dense, rk});
@@ -1484,6 +1513,7 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                                                   P<float>(h->tab), dense);
         }
         h->recHierId = h->hierId;
+        if (sideFold && (rc = hip_check(h, hipStreamWaitEvent(s, h->evFoldJoin, 0), "fold join wait"))) return rc;
         return hip_check(h, hipGetLastError(), "assembly kernels");
     }
 

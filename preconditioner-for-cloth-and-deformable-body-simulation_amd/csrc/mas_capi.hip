@@ -207,6 +207,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_FUSED_AFTER_LEVELS")) h->fusedAfterLevels = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_THREAD")) h->earlyThread = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_OD")) h->earlyOd = std::atoi(v);
+    if (const char* v = std::getenv("MAS_FOLD_SIDE")) h->foldSide = std::atoi(v);
     if (const char* v = std::getenv("MAS_HIER_CACHE")) h->hierCache = std::atoi(v);
     // MAS_PREP_SERIAL=1 (A/B) queues the early path on the caller's stream: from
     // one host thread, so the launch order on that stream is fixed
@@ -240,6 +241,12 @@ int mas_destroy(mas_handle h) {
     if (h->evPrepFork) hipEventDestroy(h->evPrepFork);
     if (h->evPrepJoin) hipEventDestroy(h->evPrepJoin);
     if (h->evAdd0) hipEventDestroy(h->evAdd0);
+    if (h->foldStream) {
+        hipStreamSynchronize(h->foldStream);
+        hipStreamDestroy(h->foldStream);
+    }
+    if (h->evFoldFork) hipEventDestroy(h->evFoldFork);
+    if (h->evFoldJoin) hipEventDestroy(h->evFoldJoin);
     for (auto& e : h->evFine)
         if (e) hipEventDestroy(e);
     release_comm(h);  // drained above; the communicator goes before the buffers it wrote

@@ -251,6 +251,11 @@ struct mas_context {
     bool odDone = false;       // this Prepare's od / record counts are queued already
     mas::FineAsm earlyFa{};    // its inputs, kept for launch_level0_fused
     hipEvent_t evAdd0 = nullptr;
+    // the cached CSR records' fold beside od / k_diag1 / the table folds
+    // (run_assemble; env MAS_FOLD_SIDE): -1 = for a sharded Prepare only
+    int foldSide = -1;
+    hipStream_t foldStream = nullptr;
+    hipEvent_t evFoldFork = nullptr, evFoldJoin = nullptr;
     mas::Buffer add0, c0Cnt, c0Off, c0Keys, c0KeysS, c0Ids, c0IdsS, c0Val, a0Keys, a0KeysS, a0Ids, a0IdsS, a0Val;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, tab, termCnt;
