@@ -19,6 +19,9 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     int rc;
     h->prepared = false;
     h->err.clear();  // after a successful Prepare: empty, or the non-SPD warning
+    // a previous Prepare that failed between the side fold's fork and join
+    // (run_assemble) may have left it running: this Prepare's memsets wait
+    if (h->foldStream) hipStreamWaitEvent(s, h->evFoldJoin, 0);
     hipEventRecord(h->ev[2], s);
     // pivot checks of this Prepare's factors: [0] count, [1] lowest block (k_factor.hip check_pivots)
     int* status = P<int>(h->devStatus);
