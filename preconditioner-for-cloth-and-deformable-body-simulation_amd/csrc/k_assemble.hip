@@ -956,7 +956,15 @@ __global__ __launch_bounds__(256) void k_term_write_lanes(int l, int nV, const i
     if (l == 2 && j == 0) terms[o + __popcll(grp)] = -(u + 1);
 }
 
-constexpr int kFoldChunk = 512, kFoldStride = kFoldChunk + 4;
+// Terms per staged chunk of k_table_fold (a compile-time A/B knob): 256
+// against 512 / 1024 / 128, world-8 rank at 1M + contacts 1.29 -> 1.24 ms,
+// 4M tet rank 3.70 -> 3.6 (the 9.4 KB of LDS per node leaves room for more
+// nodes per CU; 1024 was slower everywhere, 128 the same as 256;
+// profiles/round5/ab/table_fold_chunk/)
+#ifndef MAS_FOLD_CHUNK
+#define MAS_FOLD_CHUNK 256
+#endif
+constexpr int kFoldChunk = MAS_FOLD_CHUNK, kFoldStride = kFoldChunk + 4;
 
 __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, int beginPrev,
                                                    const int* __restrict__ vlist, const int* __restrict__ voff,

@@ -1,0 +1,19 @@
+# Round 5: table fold chunk 1024 (and 256) vs 512: block-bitwise
+# tests, then steady-state Prepare alternating with the previous build.
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r5ai; mkdir -p $O; export TMPDIR=/tmp
+cd $R || exit 1
+true && \
+    > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for rep in 1 2 3; do
+  for lib in libmas_amd_ab_fc1024.so libmas_amd.so libmas_amd_ab_fc256.so; do
+    for sh in "" "3,8"; do
+      for c in 1M+contacts 4M-tet; do
+        tag=${lib}_${c}_${sh/,/of}_$rep
+        PREP_SHARD=$sh MAS_LIB_NAME=$lib timeout -k 10 300 python3 scripts/dev/prep_only.py $c 6 > $O/prep_$tag.log 2>&1 || { tail -5 $O/prep_$tag.log; exit 1; }
+        echo "$tag: $(grep -o 'prepare [0-9.]* ms\|from [0-9.]*' $O/prep_$tag.log | tail -6 | tr '\n' ' ')"
+      done
+    done
+  done
+done
