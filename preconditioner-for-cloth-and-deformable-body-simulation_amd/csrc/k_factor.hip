@@ -753,7 +753,19 @@ int run_factor(mas_context* h, hipStream_t s) {
     // the prepared level-0 blocks (all, or a shard's; the fused variant factored
     // them already, on prepStream), then every coarse block
     const bool fused = h->factorVariant >= 4;
+#ifdef MAS_TIMING_OWN_COARSE
+    // timing probe only (other ranks' level-1 inverses stay stale): on a sharded
+    // Prepare a rank factors its equal share of the level-1 blocks and every
+    // block of levels >= 2, as the planned sharded coarse assembly would
+    const int n1b = (h->levelSize[2] + 31) / 32;
+    const int own0 = h->prepWorld > 1 ? h->nFineBlk + (int)((long long)h->prepRank * n1b / h->prepWorld) : h->nFineBlk;
+    const int own1 = h->prepWorld > 1 ? h->nFineBlk + (int)((long long)(h->prepRank + 1) * n1b / h->prepWorld)
+                                      : h->nFineBlk + n1b;
+    const int ranges[3][2] = {{h->fineBlk0, fused ? h->fineBlk0 : h->fineBlk1}, {own0, own1},
+                              {h->nFineBlk + n1b, h->nBlk}};
+#else
     const int ranges[2][2] = {{h->fineBlk0, fused ? h->fineBlk0 : h->fineBlk1}, {h->nFineBlk, h->nBlk}};
+#endif
     for (const auto& rg : ranges) {
         const int b0 = rg[0], nb = rg[1] - rg[0];
         if (nb <= 0) continue;
