@@ -773,7 +773,11 @@ int run_factor(mas_context* h, hipStream_t s) {
             k_factor<<<nb, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv, b0, P<int>(h->devStatus));
         } else {
             k_identity_fix<<<cdiv(nb * 32, 256), 256, 0, s>>>(dense, b0 * 32, rg[1] * 32);
+#ifdef MAS_AB_COARSE_MFMA
+            if (h->factorVariant == 3 || (h->factorVariant == 5 && b0 >= h->nFineBlk))
+#else
             if (h->factorVariant == 3)
+#endif
                 k_factor_rb<true><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0,
                                                     P<int>(h->devStatus));
             else
