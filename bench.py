@@ -584,9 +584,9 @@ def main():
                                  "assemble": round(st0["prepare_assemble_ms"], 3),
                                  "factor": round(st0["prepare_factor_ms"], 3),
                                  "level0_fused_overlapped": round(st0["prepare_fine_ms"], 3)},
-        "factor_formation": ("level-0 inverses Inv = L^-T D^-1 L^-1 on the matrix cores (v_mfma_f32_32x32x2_f32)"
+        "factor_formation": ("level-0 and coarse inverses Inv = L^-T D^-1 L^-1 on the matrix cores (v_mfma_f32_32x32x2_f32)"
                              if st0.get("factor_formation") == 1 else
-                             "level-0 inverses in the reference's operation order on the vector ALUs"),
+                             "level-0 and coarse inverses in the reference's operation order on the vector ALUs"),
         # the handle's mas_config switches (include/mas_capi.h): 0 = the tolerance-mode defaults (z within
         # 1e-5 of the reference arithmetic), 1 = the reference's own operation order, bitwise
         "mas_config": {"reference_formation": 0, "reference_restriction": 0},

@@ -773,11 +773,11 @@ int run_factor(mas_context* h, hipStream_t s) {
             k_factor<<<nb, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv, b0, P<int>(h->devStatus));
         } else {
             k_identity_fix<<<cdiv(nb * 32, 256), 256, 0, s>>>(dense, b0 * 32, rg[1] * 32);
-#ifdef MAS_AB_COARSE_MFMA
-            if (h->factorVariant == 3 || (h->factorVariant == 5 && b0 >= h->nFineBlk))
-#else
-            if (h->factorVariant == 3)
-#endif
+            // the matrix-core formation for the coarse blocks too unless the
+            // reference's order is asked for (variant 4): 0.125 -> 0.104 ms at
+            // 1M + contacts, coarse inverses within 4.4e-8 relative
+            // (profiles/round5/ab/coarse_formation/)
+            if (h->factorVariant == 3 || h->factorVariant == 5)
                 k_factor_rb<true><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0,
                                                     P<int>(h->devStatus));
             else

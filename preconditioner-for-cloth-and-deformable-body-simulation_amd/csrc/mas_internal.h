@@ -173,8 +173,8 @@ struct mas_context {
     // LDS slabs + register-blocked factor, one kernel, overlapped with the
     // coarse assembly on prepStream); 2 = k_level0_block + k_factor_rb;
     // 3 = 2 with the MFMA formation (not bitwise); 5 = 4 with the MFMA
-    // formation (not bitwise, the default; mas_config.reference_formation = 1
-    // selects 4); 0 = LDS-row k_factor
+    // formation, level 0 and the coarse blocks (not bitwise, the default;
+    // mas_config.reference_formation = 1 selects 4); 0 = LDS-row k_factor
     int factorVariant = 5;
     // coarse levels (env MAS_COARSE_MODE): 3 = one launch with tagged
     // hand-offs (k_coarse1.hip, L >= 3); 2 = two launches, restrictions then
