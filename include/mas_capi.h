@@ -81,8 +81,9 @@ typedef struct {
     int keep_blocks;   /* 1 = Prepare also stores the assembled level-0 blocks (mas_get_block_matrix on
                           them; +2.4 GB of HBM traffic at 1M).  0 = the fused level-0 assemble + factor
                           never writes them; only the coarse blocks are kept */
-    int reference_formation; /* 0 = the level-0 inverses Inv = L^-T D^-1 L^-1 are formed on the matrix
-                                cores (default; within 5e-8 of the reference arithmetic, not bitwise);
+    int reference_formation; /* 0 = every block's inverse Inv = L^-T D^-1 L^-1 (level 0 and coarse) is
+                                formed on the matrix cores (default; within 5e-8 of the reference
+                                arithmetic, not bitwise);
                                 1 = the reference's own operation order on the vector ALUs
                                 (.cpp:1437-1495): every inverse bitwise equal to the reference
                                 arithmetic, ~0.15 ms more Prepare at 1M */
