@@ -52,7 +52,11 @@ extern "C" {
  *    counts the blocks in mas_stats.nonspd_blocks and leaves a warning in
  *    mas_last_error, as the reference keeps going.  mas_apply_device reports
  *    an earlier apply's coarse give-up (MAS_ERR_HIP) before queueing. */
-#define MAS_ABI_VERSION 4
+/* 5: the sharded coarse assembly (mas_prepare_shard_rows / _complete,
+ *    mas_set_prepare_allgather; mas_stats.prepare_complete_ms and coarse_split
+ *    from the reserved tail, same size); mas_allgather_loopback; the sharded
+ *    apply's coarse levels run on the communication stream. */
+#define MAS_ABI_VERSION 5
 
 typedef enum {
     MAS_OK = 0,
@@ -72,6 +76,8 @@ typedef enum {
 } mas_status;
 
 typedef struct mas_context* mas_handle;
+/* an allgather of `bytes` per rank (see mas_shard_apply_device) */
+typedef int (*mas_allgather_fn)(const void* send, void* recv, size_t bytes, void* stream, void* user);
 
 typedef struct {
     int max_levels;    /* 0 = reference rule (ComputeLevelNums .cpp:112-135), else min(natural, max_levels) */
@@ -149,7 +155,11 @@ typedef struct {
                                   stream (no device-wide sync).  The apply that gave up is named by
                                   MAS_ERR_HIP from mas_apply / the PCG solve itself, or for mas_apply_device
                                   from the next mas_apply* / PCG call on the handle */
-    int64_t reserved[3];       /* zero; room for later fields without a size change */
+    double prepare_complete_ms; /* ABI 5: device time of the last mas_prepare_shard_complete (unpack + factor) */
+    int64_t coarse_split;      /* ABI 5: the last Prepare's coarse assembly: 0 = every row (unsharded),
+                                  1 = sharded, own rows only (the split cuts no subtree), 2 = sharded, every
+                                  row (the split cuts a subtree); 1 and 2 exchange rows the same way */
+    int64_t reserved[1];       /* zero; room for later fields without a size change */
 } mas_stats;
 
 /* lifecycle */
@@ -263,6 +273,26 @@ int mas_shard_plan(int nV, const int* l1_first, int rank, int world, mas_shard* 
  * the PCG driver and mas_save_blob then fail with MAS_ERR_STATE.  (0, 1)
  * restores the whole Prepare. */
 int mas_set_prepare_shard(mas_handle h, int rank, int world);
+/* ABI 5.  The sharded coarse assembly.  A
+ * sharded Prepare (world > 1, L >= 2) assembles only the coarse rows whose
+ * subtree lies in its Morton range (every row when the equal split cuts a
+ * subtree: mas_stats.coarse_split = 2), factors the level-1 blocks only it has
+ * rows in, and leaves the rows other ranks need in one device segment:
+ *   mas_prepare_shard_rows      -> that segment and its size (the same on
+ *                                  every rank: the largest rank's, padded)
+ *   caller: allgather the segments into d_gathered[world][seg_bytes]
+ *   mas_prepare_shard_complete  -> unpack the other ranks' rows, factor the
+ *                                  shared level-1 blocks and every level >= 2
+ *                                  block; synchronous; then the handle serves
+ *                                  the sharded apply (before it: MAS_ERR_STATE).
+ * Every inverse the rank's sharded apply reads is then bitwise the unsharded
+ * Prepare's.  The exchange runs inside mas_prepare instead (nothing pending)
+ * when the handle has an RCCL communicator of the same rank / world
+ * (mas_rccl_init before the Prepare) or an allgather hook registered here
+ * (fn NULL: none). */
+int mas_set_prepare_allgather(mas_handle h, mas_allgather_fn fn, void* user);
+int mas_prepare_shard_rows(mas_handle h, void** d_seg, size_t* seg_bytes);
+int mas_prepare_shard_complete(mas_handle h, const void* d_gathered, void* stream);
 /* The same plan for a prepared handle. */
 int mas_shard_setup(mas_handle h, int rank, int world, mas_shard* out);
 int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r4, float* d_seg4, void* stream);
@@ -296,9 +326,14 @@ int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_g
  * nonzero on failure (reported as MAS_ERR_COMM).  It is called from the
  * calling thread during mas_shard_apply_device; `user` is passed through.
  * allgather may be NULL only when world == 1. */
-typedef int (*mas_allgather_fn)(const void* send, void* recv, size_t bytes, void* stream, void* user);
+/* (mas_allgather_fn is declared next to mas_handle above) */
 int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn allgather, void* user, float* d_z4,
                            const float* d_r4, void* stream);
+/* ABI 5.  A one-process stand-in for the collective (tests, per-rank timing
+ * on one GPU): copies `send` into slot *(const int*)user of `recv` on
+ * `stream`; the other slots are left unchanged.  Pass it as `allgather` with
+ * user = &rank. */
+int mas_allgather_loopback(const void* send, void* recv, size_t bytes, void* stream, void* user);
 
 /* The same over RCCL (xGMI) with a communicator the handle owns.  RCCL is
  * loaded at run time (librccl.so.1; the one already in the process if any).
@@ -342,6 +377,9 @@ int mas_get_neighbors(mas_handle h, int* nbr_num, int* nbr);
  * and its inverse unpacked to 96x96. */
 int mas_get_block_matrix(mas_handle h, int blk, float* out96x96);
 int mas_get_block_inverse(mas_handle h, int blk, float* out96x96);
+/* ABI 5.  Blocks [blk0, blk0 + nblk)'s inverses as stored (4 656 floats each,
+ * the packed layout of csrc/layout.h), for bitwise comparisons. */
+int mas_get_packed_inverses(mas_handle h, int blk0, int nblk, float* out);
 /* The residual hierarchy of the most recent single-GPU apply
  * (BuildResidualHierarchy .cpp:1548-1598) as out4[total_clusters - begin_1][4]
  * over coarse node ids begin_1 .. total_clusters-1.  Only levels

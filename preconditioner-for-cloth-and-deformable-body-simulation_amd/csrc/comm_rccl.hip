@@ -67,6 +67,12 @@ static int rccl_allgather(const void* send, void* recv, size_t bytes, void* stre
     return 0;
 }
 
+int comm_allgather(mas_context* h, const void* send, void* recv, size_t bytes, hipStream_t s) {
+    if (!h->rcclComm || !rccl().ok()) return fail(h, MAS_ERR_STATE, "no RCCL communicator (mas_rccl_init)");
+    if (rccl_allgather(send, recv, bytes, s, h)) return fail(h, MAS_ERR_COMM, h->err);
+    return MAS_OK;
+}
+
 }  // namespace mas
 
 using namespace mas;

@@ -180,9 +180,13 @@ __device__ __forceinline__ int climb_nodes(const unsigned (&nd)[5][5], int x, in
 // counts: dCnt[i] block-entry records, aCnt[i] additional records of stencil i
 // skip0: without the level-0 records (block entries of same-bank pairs, the
 // w^2 additional rows), which run_level0_early built already
+// own: the rows this Prepare assembles (every row unless the coarse
+// assembly is split over shards, coarse_split.hip): a record whose target row
+// (block entry: its row node; additional: its node) is another rank's is not
+// written
 __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restrict__ st, int n,
                                                        const int4* __restrict__ anc, int L, int* __restrict__ dCnt,
-                                                       int* __restrict__ aCnt, bool skip0) {
+                                                       int* __restrict__ aCnt, bool skip0, OwnNodes own) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
     if (i == n) {  // closes the exclusive scans
@@ -192,7 +196,9 @@ __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restr
     const DevStencil s = st[i];
     unsigned nd[5][5];
     stencil_nodes(s, anc, nd);
-    int d = 0, a = skip0 ? 0 : s.n;
+    int d = 0, a = 0;
+    if (!skip0)
+        for (int it = 0; it < s.n; ++it) a += own.own((unsigned)s.idx[it]);
 #pragma unroll
     for (int x = 0; x < 5; ++x)
 #pragma unroll
@@ -201,8 +207,11 @@ __global__ __launch_bounds__(256) void k_contact_count(const DevStencil* __restr
             unsigned my = 0, ot = 0;
             const int level = climb_nodes(nd, x, y, L, my, ot);
             if (level >= L) continue;
-            if (level > 0 || !skip0) d += 2;
-            if (level < L - 1) a += nd[x][level + 1] == nd[y][level + 1] ? 1 : 2;
+            if (level > 0 || !skip0) d += (int)own.own(my) + (int)own.own(ot);
+            if (level < L - 1) {
+                const unsigned pm = nd[x][level + 1], po = nd[y][level + 1];
+                a += pm == po ? (int)own.own(pm) : (int)own.own(pm) + (int)own.own(po);
+            }
         }
     dCnt[i] = d;
     aCnt[i] = a;
@@ -217,7 +226,8 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
                                                        EntryKey* __restrict__ dKeys, int* __restrict__ dIds,
                                                        float* __restrict__ dVal, int* __restrict__ dEnt,
                                                        unsigned* __restrict__ aKeys, int* __restrict__ aIds,
-                                                       float* __restrict__ aVal, bool skip0, unsigned kb) {
+                                                       float* __restrict__ aVal, bool skip0, unsigned kb,
+                                                       OwnNodes own) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const DevStencil s = st[i];
@@ -226,10 +236,12 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
     float hm[9];
     contact_h(s, hm);
     int d = dOff[i], a = aOff[i];
-    for (int it = 0; it < s.n && !skip0; ++it, ++a) {  // .cpp:1214-1217: additional[idx] += h w^2
+    for (int it = 0; it < s.n && !skip0; ++it) {  // .cpp:1214-1217: additional[idx] += h w^2
+        if (!own.own((unsigned)s.idx[it])) continue;
         aKeys[a] = (unsigned)s.idx[it];
         aIds[a] = a;
         contact_self(hm, s.w[it], aVal + 9 * (size_t)a);
+        ++a;
     }
 #pragma unroll
     for (int x = 0; x < 5; ++x)
@@ -244,29 +256,34 @@ __global__ __launch_bounds__(256) void k_contact_write(const DevStencil* __restr
             if (level > 0 || !skip0) {
                 // pDenseHessian[ot % bank][my] (entry row my, column ot), then [my % bank][ot];
                 // rows relative to kb (begin_1 when only coarse records are written)
-                dKeys[d] = (EntryKey)(((my - kb) << 5) | (ot & 31u));
-                dKeys[d + 1] = (EntryKey)(((ot - kb) << 5) | (my & 31u));
-                dIds[d] = d;
-                dIds[d + 1] = d + 1;
-                dEnt[d] = (int)(((my & 31u) << 5) | (ot & 31u));  // FineAsm::cent (level-0 records)
-                dEnt[d + 1] = (int)(((ot & 31u) << 5) | (my & 31u));
-                for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = dVal[9 * (size_t)(d + 1) + e] = t[e];
-                d += 2;
+                const unsigned rows[2] = {my, ot}, cols[2] = {ot, my};
+                for (int hf = 0; hf < 2; ++hf) {
+                    if (!own.own(rows[hf])) continue;
+                    dKeys[d] = (EntryKey)(((rows[hf] - kb) << 5) | (cols[hf] & 31u));
+                    dIds[d] = d;
+                    dEnt[d] = (int)(((rows[hf] & 31u) << 5) | (cols[hf] & 31u));  // FineAsm::cent (level-0 records)
+                    for (int e = 0; e < 9; ++e) dVal[9 * (size_t)d + e] = t[e];
+                    ++d;
+                }
             }
             if (level < L - 1) {
                 const unsigned pm = nd[x][level + 1], po = nd[y][level + 1];
                 if (pm == po) {
-                    aKeys[a] = pm - kb;
-                    aIds[a] = a;
-                    for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = contact_double(t[e]);
-                    ++a;
+                    if (own.own(pm)) {
+                        aKeys[a] = pm - kb;
+                        aIds[a] = a;
+                        for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = contact_double(t[e]);
+                        ++a;
+                    }
                 } else {
-                    aKeys[a] = pm - kb;
-                    aKeys[a + 1] = po - kb;
-                    aIds[a] = a;
-                    aIds[a + 1] = a + 1;
-                    for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = aVal[9 * (size_t)(a + 1) + e] = t[e];
-                    a += 2;
+                    const unsigned ps[2] = {pm, po};
+                    for (int hf = 0; hf < 2; ++hf) {
+                        if (!own.own(ps[hf])) continue;
+                        aKeys[a] = ps[hf] - kb;
+                        aIds[a] = a;
+                        for (int e = 0; e < 9; ++e) aVal[9 * (size_t)a + e] = t[e];
+                        ++a;
+                    }
                 }
             }
         }
@@ -520,9 +537,10 @@ __global__ __launch_bounds__(64) void k_level0_block(int nV, int L, const int* _
 // k_level0_block's per-vertex sums without the tile (the fused variant builds
 // the tiles inside k_factor_fused).  od = diag + additional, then the
 // same-bank neighbour blocks in ELL order (.cpp:1270-1282).
-__global__ __launch_bounds__(256) void k_od(FineAsm a, float* __restrict__ od, int* __restrict__ recCnt) {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= a.nV) return;
+__global__ __launch_bounds__(256) void k_od(FineAsm a, float* __restrict__ od, int* __restrict__ recCnt, int v0,
+                                            int v1) {
+    const int v = v0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= v1) return;
     const int o = a.s2o[v];
     float acc[9];
     const float* d = a.diag9 + 9 * (size_t)o;
@@ -566,13 +584,16 @@ __global__ __launch_bounds__(256) void k_od(FineAsm a, float* __restrict__ od, i
 // the slots in ELL order (the same left fold, skipping cross-bank slots:
 // bitwise equal to k_od).
 template <int G>
-__global__ __launch_bounds__(256) void k_od_lanes(FineAsm a, float* __restrict__ od, int* __restrict__ recCnt) {
+__global__ __launch_bounds__(256) void k_od_lanes(FineAsm a, float* __restrict__ od, int* __restrict__ recCnt, int v0,
+                                                  int v1) {
     constexpr int VPW = 64 / G;  // vertices per wave
+    // lane j folds entries j and j + G: all nine only when G >= 8
+    static_assert(G >= 8 && 2 * G >= 9 && 64 % G == 0, "k_od_lanes: 8, 16, 32 or 64 lanes per vertex");
     __shared__ float stg[4][64][10];  // [wave][lane][entry], padded row
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int v = t / G, j = t % G, g0 = lane & ~(G - 1);
-    const bool vin = v < a.nV;
+    const int v = v0 + t / G, j = t % G, g0 = lane & ~(G - 1);
+    const bool vin = v < v1;
     const int vc = vin ? v : 0;
     // every load issued as early as its address allows: the s2o -> ranges ->
     // off9 chain, and beside it nbr, the vertex's diagonal (after s2o) and
@@ -645,13 +666,15 @@ struct RecKey {
 
 // one thread per vertex (neighbour counts <= 8: a 2-D cloth has ~2 cross-bank
 // neighbours per vertex, and G lanes per vertex measured 78 vs 70 us at 1M)
+// vertices [v0, v1) only: a sharded Prepare's own (the rows of every record of
+// a vertex are its ancestors, so its own rows' records are its own vertices')
 __global__ __launch_bounds__(256) void k_records_vertex(int nV, int L, RecKey rk, const int* __restrict__ s2o,
                                                  const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                  const int* __restrict__ gn, const int* __restrict__ ranges,
                                                  const int* __restrict__ recOff, EdgeRec* __restrict__ rec,
-                                                 EntryKey* __restrict__ keys, int* __restrict__ mats) {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= nV) return;
+                                                 EntryKey* __restrict__ keys, int* __restrict__ mats, int v0, int v1) {
+    const int v = v0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= v1) return;
     const int o = s2o[v];
     const int num = nbrNum[v];
     const int base = ranges[o];
@@ -691,10 +714,10 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, RecKey rk, const
                                                  const int* __restrict__ nbrNum, const int* __restrict__ nbr,
                                                  const int* __restrict__ gn, const int* __restrict__ ranges,
                                                  const int* __restrict__ recOff, EdgeRec* __restrict__ rec,
-                                                 EntryKey* __restrict__ keys, int* __restrict__ mats) {
+                                                 EntryKey* __restrict__ keys, int* __restrict__ mats, int v0, int v1) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int v = t / G, k = 1 + t % G;
-    const bool has = v < nV && k < nbrNum[v];
+    const int v = v0 + t / G, k = 1 + t % G;
+    const bool has = v < v1 && k < nbrNum[v];
     unsigned my = (unsigned)v, ot = has ? (unsigned)nbr[(size_t)k * nV + v] : (unsigned)v;
     const bool cross = has && (my >> 5) != (ot >> 5);  // same bank: level 0 (k_level0_block)
     unsigned long long grp;
@@ -838,10 +861,10 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __
 // instead of one per vertex: beside the fused kernel this kernel runs on the
 // reserved CUs and was bound by those round trips).
 __global__ __launch_bounds__(256) void k_diag1(int nV, const int* __restrict__ gn, const float* __restrict__ od,
-                                               float* __restrict__ dense) {
+                                               float* __restrict__ dense, int w0, int w1) {
     constexpr int kB = 8;
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w * 32 >= nV) return;
+    const int w = w0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= w1 || w * 32 >= nV) return;
     const int end = min(w * 32 + 32, nV);
     unsigned cur = (unsigned)gn[w * 32];
     float acc[9];
@@ -971,9 +994,9 @@ __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, 
                                                    const int* __restrict__ termOff, const int* __restrict__ terms,
                                                    const int* __restrict__ cstPrev2, const int* __restrict__ gn,
                                                    const float* __restrict__ off9, const float* __restrict__ od,
-                                                   float* __restrict__ tab, float* __restrict__ dense) {
+                                                   float* __restrict__ tab, float* __restrict__ dense, int local0) {
     __shared__ __attribute__((aligned(16))) float st[9 * kFoldStride];
-    const int local = blockIdx.x;
+    const int local = local0 + blockIdx.x;
     const int lane = threadIdx.x;
     const int P = begin + local;
     const int vb = voff[local], ve = voff[local + 1];
@@ -1161,7 +1184,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     const unsigned kb = skip0 ? (unsigned)begin1 : 0u;
     const int Bk = skip0 ? std::max(1, bit_width((unsigned)std::max(tc - begin1 - 1, 0))) : B;
     const int4* anc = P<int4>(h->coarseTables);
-    k_contact_count<<<cdiv(n + 1, 256), 256, 0, s>>>(st, n, anc, L, P<int>(h->cdCnt), P<int>(h->caCnt), skip0);
+    k_contact_count<<<cdiv(n + 1, 256), 256, 0, s>>>(st, n, anc, L, P<int>(h->cdCnt), P<int>(h->caCnt), skip0, h->own);
     if ((rc = exclusive_scan(h, P<int>(h->cdCnt), P<int>(h->cdOff), n + 1, s, "contact scan")) ||
         (rc = exclusive_scan(h, P<int>(h->caCnt), P<int>(h->caOff), n + 1, s, "contact scan")))
         return rc;
@@ -1179,7 +1202,7 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
     k_contact_write<<<cdiv(n, 256), 256, 0, s>>>(st, n, anc, L, P<int>(h->cdOff), P<int>(h->caOff),
                                                  P<EntryKey>(h->cdKeys), P<int>(h->cdIds),
                                                  P<float>(h->cdVal), P<int>(h->cdEnt), P<unsigned>(h->caKeys),
-                                                 P<int>(h->caIds), P<float>(h->caVal), skip0, kb);
+                                                 P<int>(h->caIds), P<float>(h->caVal), skip0, kb, h->own);
     if ((rc = sort_pairs(h, P<EntryKey>(h->cdKeys), P<EntryKey>(h->cdKeysS), P<int>(h->cdIds),
                          P<int>(h->cdIdsS), nD, Bk + RecKey::kLaneBits, s, "contact entry sort")) ||
         (rc = sort_pairs(h, P<unsigned>(h->caKeys), P<unsigned>(h->caKeysS), P<int>(h->caIds), P<int>(h->caIdsS), nA,
@@ -1257,12 +1280,17 @@ static int run_contacts(mas_context* h, hipStream_t s, FineContacts& fc, FineAsm
 // od and the coarse record counts (k_od / k_od_lanes): level-0 data only.
 // Lanes per vertex: the largest neighbour count (ELL slot 0 is the vertex
 // itself), a power of two.
-static void launch_od(mas_context* h, const FineAsm& fa, hipStream_t s) {
-    const int nV = h->nV, val = h->maxNbr - 1;
-    if (val <= 8) k_od_lanes<8><<<cdiv((long long)nV * 8, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
-    else if (val <= 16) k_od_lanes<16><<<cdiv((long long)nV * 16, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
-    else if (val <= 32) k_od_lanes<32><<<cdiv((long long)nV * 32, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
-    else k_od<<<cdiv(nV, 256), 256, 0, s>>>(fa, P<float>(h->od), P<int>(h->recCnt));
+// vertices [v0, v1) (a sharded Prepare with the coarse split: its own)
+static void launch_od(mas_context* h, const FineAsm& fa, hipStream_t s, int v0, int v1) {
+    const long long n = v1 - v0;
+    const int val = h->maxNbr - 1;
+    float* od = P<float>(h->od);
+    int* cnt = P<int>(h->recCnt);
+    if (n <= 0) return;
+    if (val <= 8) k_od_lanes<8><<<cdiv(n * 8, 256), 256, 0, s>>>(fa, od, cnt, v0, v1);
+    else if (val <= 16) k_od_lanes<16><<<cdiv(n * 16, 256), 256, 0, s>>>(fa, od, cnt, v0, v1);
+    else if (val <= 32) k_od_lanes<32><<<cdiv(n * 32, 256), 256, 0, s>>>(fa, od, cnt, v0, v1);
+    else k_od<<<cdiv(n, 256), 256, 0, s>>>(fa, od, cnt, v0, v1);
 }
 
 // od and the record counts in the early path (see run_level0_early)
@@ -1362,10 +1390,19 @@ int run_level0_early(mas_context* h, const float* d_diag9, const float* d_off9, 
     // of the blocks and the replicated coarse chain is the longer path, which
     // then no longer carries od: world-8 rank at 1M + contacts 1.40-1.43 ->
     // 1.37-1.39 ms (profiles/round4/prepare/shard_sweep/)
+    // A sharded Prepare (world > 1, L >= 2): od of its own vertices only --
+    // all the coarse split needs (coarse_split.hip); when the split turns out
+    // to cut a subtree, run_assemble adds the others'.  Record counts of the
+    // other vertices are zero then (no records of theirs are built).
     h->odDone = false;
     if (early_od(h)) {
-        if ((rc = hip_check(h, hipMemsetAsync(P<int>(h->recCnt) + nV, 0, 4, ps), "memset recCnt"))) return rc;
-        launch_od(h, fa, ps);
+        const bool own = h->prepWorld > 1 && h->L > 1;
+        h->odV0 = own ? 32 * h->fineBlk0 : 0;
+        h->odV1 = own ? std::min(32 * h->fineBlk1, nV) : nV;
+        if ((rc = hip_check(h, hipMemsetAsync(P<int>(h->recCnt) + (own ? 0 : nV), 0, own ? (size_t)(nV + 1) * 4 : 4, ps),
+                            "memset recCnt")))
+            return rc;
+        launch_od(h, fa, ps, h->odV0, h->odV1);
         h->odDone = true;
     }
     if ((rc = hip_check(h, hipEventRecord(h->evAdd0, ps), "add0 ready"))) return rc;
@@ -1452,8 +1489,10 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     // side fold slows that kernel (1.83 -> 1.90 ms) and Prepare 2.35-2.37 ->
     // 2.36-2.41 (profiles/round5/ab/fold_side/), so it stays in line there.
     const bool sideWanted = h->foldSide > 0 || (h->foldSide < 0 && h->prepWorld > 1);
-    const bool sideFold = L > 1 && sideWanted && h->hierCache && h->recHierId == h->hierId && !h->rangesChanged &&
-                          h->nRecCached > 0;
+    // the cached records are the own vertices' of a shard (coarse split) or everyone's
+    const long long shardKey = h->splitClean ? ((long long)h->prepRank << 32) + h->prepWorld : 0;
+    const bool recsValid = h->hierCache && h->recHierId == h->hierId && !h->rangesChanged && h->recShardKey == shardKey;
+    const bool sideFold = L > 1 && sideWanted && recsValid && h->nRecCached > 0;
     if (sideFold) {
         if (!h->foldStream && ((rc = hip_check(h, hipStreamCreateWithFlags(&h->foldStream, hipStreamNonBlocking),
                                                "fold stream")) ||
@@ -1483,7 +1522,15 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         } else if (!forked && (rc = fork_fused(h, fa, s))) {
             return rc;
         }
-        if (!h->odDone) launch_od(h, fa, s);
+        // od: the rows this Prepare assembles need it for their vertices
+        // (a sharded Prepare with the coarse split: its own; else all)
+        const int v0 = h->splitClean ? h->own.lo[0] : 0, v1 = h->splitClean ? h->own.hi[0] : nV;
+        if (!h->odDone) {
+            launch_od(h, fa, s, v0, v1);
+        } else {  // the early path covered [odV0, odV1)
+            launch_od(h, fa, s, v0, std::min(v1, h->odV0));
+            launch_od(h, fa, s, std::max(v0, h->odV1), v1);
+        }
     } else {
         k_level0_block<<<h->nFineBlk, 64, 0, s>>>(nV, L, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), d_diag9,
                                                   d_off9, d_ranges, add, dense, P<float>(h->od), P<int>(h->recCnt),
@@ -1495,8 +1542,16 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     // depend only on the hierarchy and the CSR structure, not on any value: a
     // Prepare whose hierarchy is the one they were built for (and whose CSR
     // ranges equal the ones they index off9 with) reuses them and only folds.
-    const bool cached = h->hierCache && h->recHierId == h->hierId && !h->rangesChanged;
+    const bool cached = recsValid;
     h->recHierId = ~0ull;  // valid again only once rebuilt below
+    // the banks / nodes per level this Prepare folds (a shard's own, or all)
+    const int bank0 = h->splitClean ? h->own.lo[0] / 32 : 0;
+    const int bank1 = h->splitClean ? cdiv(h->own.hi[0], 32) : h->nFineBlk;
+    auto nodeRange = [&](int l, int& local0, int& cnt) {
+        const int begin = h->levelSize[2 * l + 1], count = h->levelSize[2 * l];
+        local0 = h->splitClean ? h->own.lo[l] - begin : 0;
+        cnt = h->splitClean ? h->own.hi[l] - h->own.lo[l] : count;
+    };
     EdgeRec* rec = P<EdgeRec>(h->rec);
     const RecKey rk{h->levelSize[3], bit_width((unsigned)(tc - h->levelSize[3]))};
     if (rk.bits() > 32) return fail(h, MAS_ERR_ARG, "record keys: more than 2^27 coarse nodes");
@@ -1510,17 +1565,21 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
             k_fold_runs<DenseEntry, true, EntryKey><<<cdiv(nRec, 64), 64, 0, s>>>(
                 nRec, rk.dead(), P<EntryKey>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
                 DenseEntry{dense, rk});
-        k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
+        if (bank1 > bank0)
+            k_diag1<<<cdiv(bank1 - bank0, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense, bank0, bank1);
         for (int l = 2; l < L; ++l) {
             const int count = h->levelSize[2 * l], begin = h->levelSize[2 * l + 1];
             const int beginPrev = h->levelSize[2 * (l - 1) + 1];
-            if (count > 0)
-                k_table_fold<<<count, 64, 0, s>>>(l, count, begin, beginPrev, P<int>(h->vlistL[l]),
-                                                  P<int>(h->voffL[l]), P<int>(h->termOffL[l]), P<int>(h->termsL[l]),
-                                                  P<int>(h->cst) + (size_t)(l - 2) * nV, gn, d_off9, P<float>(h->od),
-                                                  P<float>(h->tab), dense);
+            int local0 = 0, cnt = 0;
+            nodeRange(l, local0, cnt);
+            if (cnt > 0)
+                k_table_fold<<<cnt, 64, 0, s>>>(l, count, begin, beginPrev, P<int>(h->vlistL[l]),
+                                                P<int>(h->voffL[l]), P<int>(h->termOffL[l]), P<int>(h->termsL[l]),
+                                                P<int>(h->cst) + (size_t)(l - 2) * nV, gn, d_off9, P<float>(h->od),
+                                                P<float>(h->tab), dense, local0);
         }
         h->recHierId = h->hierId;
+        h->recShardKey = shardKey;
         if (sideFold && (rc = hip_check(h, hipStreamWaitEvent(s, h->evFoldJoin, 0), "fold join wait"))) return rc;
         return hip_check(h, hipGetLastError(), "assembly kernels");
     }
@@ -1539,17 +1598,20 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
     if ((rc = hip_check(h, hipMemcpyAsync(h->recRanges.p, d_ranges, (size_t)(nV + 1) * 4, hipMemcpyDeviceToDevice, s),
                         "keep ranges")))
         return rc;
+    // the vertices whose records are built (their counts are zero elsewhere)
+    const int rv0 = h->splitClean ? h->own.lo[0] : 0, rv1 = h->splitClean ? h->own.hi[0] : nV;
     auto recordLaunch = [&](auto gtag) {
         constexpr int G = decltype(gtag)::value;
-        k_records<G><<<cdiv(nV * G, 256), 256, 0, s>>>(nV, L, rk, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr),
-                                                       gn, d_ranges, P<int>(h->recOff), rec,
-                                                       P<EntryKey>(h->recKeys), P<int>(h->recIds));
+        k_records<G><<<cdiv((long long)(rv1 - rv0) * G, 256), 256, 0, s>>>(
+            nV, L, rk, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), gn, d_ranges, P<int>(h->recOff), rec,
+            P<EntryKey>(h->recKeys), P<int>(h->recIds), rv0, rv1);
     };
     switch (lanesPerVertex) {
         case 8:
-            k_records_vertex<<<cdiv(nV, 256), 256, 0, s>>>(nV, L, rk, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr),
-                                                           gn, d_ranges, P<int>(h->recOff), rec,
-                                                           P<EntryKey>(h->recKeys), P<int>(h->recIds));
+            if (rv1 > rv0)
+                k_records_vertex<<<cdiv(rv1 - rv0, 256), 256, 0, s>>>(
+                    nV, L, rk, P<int>(h->s2o), P<int>(h->nbrNum), P<int>(h->nbr), gn, d_ranges, P<int>(h->recOff), rec,
+                    P<EntryKey>(h->recKeys), P<int>(h->recIds), rv0, rv1);
             break;
         case 16: recordLaunch(std::integral_constant<int, 16>{}); break;
         case 32: recordLaunch(std::integral_constant<int, 32>{}); break;
@@ -1563,7 +1625,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
             nRec, rk.dead(), P<EntryKey>(h->recKeysSorted), P<int>(h->recIdsSorted), d_off9,
             DenseEntry{dense, rk});
     }
-    k_diag1<<<cdiv(h->nFineBlk, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense);
+    if (bank1 > bank0)
+        k_diag1<<<cdiv(bank1 - bank0, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense, bank0, bank1);
 
     // diagTable folds, levels 2..L-1 (term lists kept per level for the next Prepare)
     if ((rc = ensure(h, h->vkeys, (size_t)nV * 4)) || (rc = ensure(h, h->termCnt, (size_t)(nV + 1) * 4))) return rc;
@@ -1605,12 +1668,15 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                                                                           termOff, terms);
                 break;
         }
-        if (count > 0)
-            k_table_fold<<<count, 64, 0, s>>>(l, count, begin, beginPrev, vlist, voff, termOff, terms, cstPrev2, gn,
-                                              d_off9, P<float>(h->od), P<float>(h->tab), dense);
+        int local0 = 0, cnt = 0;
+        nodeRange(l, local0, cnt);
+        if (cnt > 0)
+            k_table_fold<<<cnt, 64, 0, s>>>(l, count, begin, beginPrev, vlist, voff, termOff, terms, cstPrev2, gn,
+                                            d_off9, P<float>(h->od), P<float>(h->tab), dense, local0);
     }
     h->nRecCached = nRec;
     h->recHierId = h->hierId;
+    h->recShardKey = shardKey;
     return hip_check(h, hipGetLastError(), "assembly kernels");
 }
 

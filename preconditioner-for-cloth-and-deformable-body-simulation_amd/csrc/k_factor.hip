@@ -747,45 +747,43 @@ int copy_block_inverse(mas_context* h, int blk, float* out96) {
     return MAS_OK;
 }
 
-int run_factor(mas_context* h, hipStream_t s) {
+int factor_blocks(mas_context* h, int b0, int b1, hipStream_t s) {
+    const int nb = b1 - b0;
+    if (nb <= 0) return MAS_OK;
     float* dense = dense_base(h);
     float* inv = P<float>(h->inv);
-    // the prepared level-0 blocks (all, or a shard's; the fused variant factored
-    // them already, on prepStream), then every coarse block
-    const bool fused = h->factorVariant >= 4;
-#ifdef MAS_TIMING_OWN_COARSE
-    // timing probe only (other ranks' level-1 inverses stay stale): on a sharded
-    // Prepare a rank factors its equal share of the level-1 blocks and every
-    // block of levels >= 2, as the planned sharded coarse assembly would
-    const int n1b = (h->levelSize[2] + 31) / 32;
-    const int own0 = h->prepWorld > 1 ? h->nFineBlk + (int)((long long)h->prepRank * n1b / h->prepWorld) : h->nFineBlk;
-    const int own1 = h->prepWorld > 1 ? h->nFineBlk + (int)((long long)(h->prepRank + 1) * n1b / h->prepWorld)
-                                      : h->nFineBlk + n1b;
-    const int ranges[3][2] = {{h->fineBlk0, fused ? h->fineBlk0 : h->fineBlk1}, {own0, own1},
-                              {h->nFineBlk + n1b, h->nBlk}};
-#else
-    const int ranges[2][2] = {{h->fineBlk0, fused ? h->fineBlk0 : h->fineBlk1}, {h->nFineBlk, h->nBlk}};
-#endif
-    for (const auto& rg : ranges) {
-        const int b0 = rg[0], nb = rg[1] - rg[0];
-        if (nb <= 0) continue;
-        if (h->factorVariant == 0) {
-            k_factor<<<nb, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv, b0, P<int>(h->devStatus));
-        } else {
-            k_identity_fix<<<cdiv(nb * 32, 256), 256, 0, s>>>(dense, b0 * 32, rg[1] * 32);
-            // the matrix-core formation for the coarse blocks too unless the
-            // reference's order is asked for (variant 4): 0.125 -> 0.104 ms at
-            // 1M + contacts, coarse inverses within 4.4e-8 relative
-            // (profiles/round5/ab/coarse_formation/)
-            if (h->factorVariant == 3 || h->factorVariant == 5)
-                k_factor_rb<true><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0,
-                                                    P<int>(h->devStatus));
-            else
-                k_factor_rb<false><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0,
-                                                     P<int>(h->devStatus));
-        }
+    if (h->factorVariant == 0) {
+        k_factor<<<nb, kFactorThreads, 0, s>>>(dense, P<unsigned>(h->slotTable), inv, b0, P<int>(h->devStatus));
+    } else {
+        k_identity_fix<<<cdiv(nb * 32, 256), 256, 0, s>>>(dense, b0 * 32, b1 * 32);
+        // the matrix-core formation for the coarse blocks too unless the
+        // reference's order is asked for (variant 4): 0.125 -> 0.104 ms at
+        // 1M + contacts, coarse inverses within 4.4e-8 relative
+        // (profiles/round5/ab/coarse_formation/)
+        if (h->factorVariant == 3 || h->factorVariant == 5)
+            k_factor_rb<true><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0,
+                                                P<int>(h->devStatus));
+        else
+            k_factor_rb<false><<<nb, 64, 0, s>>>(dense, inv, P<uint4>(h->tileSlot), P<uint4>(h->valuSlot), b0,
+                                                 P<int>(h->devStatus));
     }
-    return hip_check(h, hipGetLastError(), "factor kernel");  // run_prepare joins the fused kernel
+    return hip_check(h, hipGetLastError(), "factor kernel");
+}
+
+int run_factor(mas_context* h, hipStream_t s) {
+    // the prepared level-0 blocks (all, or a shard's; the fused variant factored
+    // them already, on prepStream), then the coarse blocks: every one, or on a
+    // Prepare with the coarse exchange those the rank alone has rows in (the
+    // rest after the exchange, complete_coarse_rows)
+    const bool fused = h->factorVariant >= 4;
+    int rc;
+    if (!fused && (rc = factor_blocks(h, h->fineBlk0, h->fineBlk1, s))) return rc;
+    if (h->splitPlanned) {
+        for (size_t i = 0; i + 1 < h->splitPre.size(); i += 2)
+            if ((rc = factor_blocks(h, h->splitPre[i], h->splitPre[i + 1], s))) return rc;
+        return MAS_OK;
+    }
+    return factor_blocks(h, h->nFineBlk, h->nBlk, s);  // run_prepare joins the fused kernel
 }
 
 }  // namespace mas

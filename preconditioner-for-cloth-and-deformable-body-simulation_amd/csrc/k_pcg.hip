@@ -673,8 +673,10 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     float4* z = r + nV;
     float4* p = z + nV;
     float4* ap = p + nV;
-    X64* x64 = reinterpret_cast<X64*>(ap + nV);
-    float4* p2 = reinterpret_cast<float4*>(x64 + nV);  // the fused form's p of odd iterations
+    // the fused form's p of odd iterations, before x64: every float4 vector at
+    // a 16-byte offset whatever nV is (x64 is 24 B per vertex)
+    float4* p2 = ap + nV;
+    X64* x64 = reinterpret_cast<X64*>(p2 + nV);
     const bool fuseP = h->pcgFuseP;
     double* part = P<double>(h->pcgPartial);
     const int* idx = P<int>(h->idx);

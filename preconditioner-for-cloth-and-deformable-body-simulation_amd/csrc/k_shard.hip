@@ -234,6 +234,11 @@ __global__ __launch_bounds__(kApplyThreads) void k_shard_coarse12(
     }
 }
 
+__global__ __launch_bounds__(256) void k_copy16(const float4* __restrict__ src, float4* __restrict__ dst, size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
 int compute_l1_first(mas_context* h, hipStream_t s) {
     const int nb = h->nFineBlk;
     h->l1First.assign(nb + 1, 0);
@@ -255,6 +260,9 @@ int compute_l1_first(mas_context* h, hipStream_t s) {
 }  // namespace mas
 
 using namespace mas;
+
+static const char* const kRowsPending =
+    "sharded Prepare: its coarse rows were not exchanged yet (mas_prepare_shard_rows / mas_prepare_shard_complete)";
 
 extern "C" {
 
@@ -289,6 +297,7 @@ int mas_shard_setup(mas_handle h, int rank, int world, mas_shard* out) {
 int mas_apply_shard_restrict(mas_handle h, int rank, int world, const float* d_r4, float* d_seg4, void* stream) {
     if (!h || !d_r4 || !d_seg4) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    if (h->rowsPending) return fail(h, MAS_ERR_STATE, kRowsPending);
     hipSetDevice(h->device);  // ensure() allocates on the current device (shard_coarse's tables)
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
@@ -355,6 +364,7 @@ int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gat
                            float* d_z4, void* stream) {
     if (!h || !d_gathered4 || !d_r4 || !d_z4) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    if (h->rowsPending) return fail(h, MAS_ERR_STATE, kRowsPending);
     hipSetDevice(h->device);  // ensure() allocates on the current device (shard_coarse's tables)
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
@@ -380,6 +390,7 @@ int mas_apply_shard_finish(mas_handle h, int rank, int world, const float* d_gat
 int mas_apply_shard_fine(mas_handle h, int rank, int world, const float* d_r4, float* d_z4, void* stream) {
     if (!h || !d_r4 || !d_z4) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    if (h->rowsPending) return fail(h, MAS_ERR_STATE, kRowsPending);
     hipSetDevice(h->device);  // ensure() allocates on the current device (shard_coarse's tables)
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
@@ -402,6 +413,7 @@ int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_g
                              void* stream) {
     if (!h || !d_gathered4 || !d_z4) return MAS_ERR_ARG;
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    if (h->rowsPending) return fail(h, MAS_ERR_STATE, kRowsPending);
     hipSetDevice(h->device);  // ensure() allocates on the current device (shard_coarse's tables)
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
@@ -418,10 +430,14 @@ int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_g
 }
 
 // The whole per-rank apply with the collective inside (include/mas_capi.h):
-// restrict on `stream`, the allgather hook on the handle's communication
-// stream (which waits for the restrict), the own level-0 blocks on `stream`
-// meanwhile, then `stream` waits for the gather and runs the coarse levels and
-// the prolongation.  One rank has nothing to hide: the serial form.
+// restrict on `stream`, then on the handle's communication stream (which
+// waits for the restrict) the allgather hook and right behind it the coarse
+// levels (k_shard_coarse12 needs only the gathered R1), while `stream` solves
+// the own level-0 blocks; `stream` waits for the coarse levels only before the
+// prolongation.  (Round 5 ran the coarse launch on `stream` after the level-0
+// solves it does not depend on: 15.2 us of replicated coarse work after them
+// per world-8 rank at 1M + contacts.)  One rank has nothing to hide: the
+// serial form.
 int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn allgather, void* user, float* d_z4,
                            const float* d_r4, void* stream) {
     if (!h) return MAS_ERR_ARG;
@@ -430,6 +446,7 @@ int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn a
         return fail(h, MAS_ERR_ARG, "mas_shard_apply_device: vectors must be 16-byte aligned");
     if (!allgather && world != 1) return fail(h, MAS_ERR_ARG, "mas_shard_apply_device: no allgather for world > 1");
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "apply before prepare");
+    if (h->rowsPending) return fail(h, MAS_ERR_STATE, kRowsPending);
     hipSetDevice(h->device);
     mas_shard sh;
     int rc = mas_shard_setup(h, rank, world, &sh);
@@ -437,7 +454,11 @@ int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn a
     const size_t segBytes = (size_t)sh.seg_max * 16;
     if ((rc = ensure(h, h->shardSeg, segBytes)) || (rc = ensure(h, h->shardGathered, segBytes * world))) return rc;
     if (!h->commStream) {
-        if ((rc = hip_check(h, hipStreamCreateWithFlags(&h->commStream, hipStreamNonBlocking), "comm stream")) ||
+        // the coarse levels run on it beside the level-0 solves: the higher
+        // priority lets their workgroups in ahead of the solves' remaining ones
+        int lo = 0, hi = 0;
+        hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if ((rc = hip_check(h, hipStreamCreateWithPriority(&h->commStream, hipStreamNonBlocking, hi), "comm stream")) ||
             (rc = hip_check(h, hipEventCreateWithFlags(&h->evRestrict, hipEventDisableTiming), "event")) ||
             (rc = hip_check(h, hipEventCreateWithFlags(&h->evGathered, hipEventDisableTiming), "event")) ||
             (rc = hip_check(h, hipEventCreateWithFlags(&h->evShardDone, hipEventDisableTiming), "event")))
@@ -470,11 +491,37 @@ int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn a
         return rc;
     if (int e = allgather(seg, gathered, segBytes, h->commStream, user))
         return fail(h, MAS_ERR_COMM, "allgather hook returned " + std::to_string(e));
+    // the coarse levels on the communication stream, behind the gather
+    // (env MAS_SHARD_COARSE_SIDE=0: on `stream` after the level-0 solves, A/B)
+    const bool side = h->shardCoarseSide != 0;
+    if (side && h->L > 1 && (rc = shard_coarse(h, sh, world, gathered, h->commStream))) return rc;
     if ((rc = hip_check(h, hipEventRecord(h->evGathered, h->commStream), "record")) ||
         (rc = mas_apply_shard_fine(h, rank, world, d_r4, d_z4, s)) ||
-        (rc = hip_check(h, hipStreamWaitEvent(s, h->evGathered, 0), "gather wait")))
+        (rc = hip_check(h, hipStreamWaitEvent(s, h->evGathered, 0), "coarse wait")))
         return rc;
-    return mas_apply_shard_complete(h, rank, world, gathered, d_z4, s);
+    if (!side && h->L > 1 && (rc = shard_coarse(h, sh, world, gathered, s))) return rc;
+    if (h->L > 1) launch_prolong(h, sh.vert_begin, sh.vert_end, reinterpret_cast<float4*>(d_z4), s);
+    if (h->shardPendingEv) hipEventRecord(h->shardPendingEv[3], s);
+    h->shardPendingEv = nullptr;
+    h->stats.apply_calls++;
+    return hip_check(h, hipGetLastError(), "shard apply");
+}
+
+// A one-process stand-in for the allgather (mas_allgather_fn): copies this
+// rank's segment into its own slot of recv (user = const int* rank).  For
+// per-rank timing and tests on one GPU; the other ranks' slots are left as
+// they are.
+int mas_allgather_loopback(const void* send, void* recv, size_t bytes, void* stream, void* user) {
+    if (!send || !recv || !user || (bytes & 15)) return 1;
+    const int rank = *static_cast<const int*>(user);
+    // a copy kernel, as a collective's would be (hipMemcpyAsync may go to a
+    // DMA engine, whose start-up latency a timing run would then measure)
+    const size_t n = bytes / 16;
+    if (n > 0)
+        k_copy16<<<cdiv((long long)n, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(
+            static_cast<const float4*>(send), reinterpret_cast<float4*>(static_cast<char*>(recv) + (size_t)rank * bytes),
+            n);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
 }  // extern "C"

@@ -209,6 +209,8 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_EARLY_OD")) h->earlyOd = std::atoi(v);
     if (const char* v = std::getenv("MAS_FOLD_SIDE")) h->foldSide = std::atoi(v);
     if (const char* v = std::getenv("MAS_HIER_CACHE")) h->hierCache = std::atoi(v);
+    if (const char* v = std::getenv("MAS_HOST_REGISTER")) h->hostRegister = std::atoi(v);
+    if (const char* v = std::getenv("MAS_SHARD_COARSE_SIDE")) h->shardCoarseSide = std::atoi(v);
     // MAS_PREP_SERIAL=1 (A/B) queues the early path on the caller's stream: from
     // one host thread, so the launch order on that stream is fixed
     if (const char* v = std::getenv("MAS_PREP_SERIAL"))
@@ -250,6 +252,8 @@ int mas_destroy(mas_handle h) {
     for (auto& e : h->evFine)
         if (e) hipEventDestroy(e);
     release_comm(h);  // drained above; the communicator goes before the buffers it wrote
+    for (auto& q : h->pins)
+        if (q.registered) hipHostUnregister(const_cast<void*>(q.p));
     h->for_each_buffer([](Buffer& b) { release(b); });
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
@@ -290,6 +294,28 @@ int mas_allocate(mas_handle h, int nV, int nE, int nF, const float* pos4, const 
     return run_allocate(h, pos4, nbr_starts, nbr_idx, edges4, faces4);
 }
 
+// Page-lock the caller's host array of slot `slot` (mas_context::pins) so the
+// copies of the host-pointer entry points run at the pinned rate instead of
+// through the runtime's pageable staging.  Memory that is pinned already
+// (hipHostMalloc, a torch pinned tensor) or cannot be registered is used as
+// it is: registration only changes the copy rate, never the result.
+static void pin_host(mas_context* h, int slot, const void* p, size_t bytes) {
+    if (!h->hostRegister || !p || !bytes) return;
+    auto& q = h->pins[slot];
+    if (q.p == p && q.bytes == bytes) return;
+    if (q.registered) hipHostUnregister(const_cast<void*>(q.p));
+    q.p = p;
+    q.bytes = bytes;
+    q.registered = false;
+    for (const auto& o : h->pins)  // one registration per array (z and r may be one buffer)
+        if (&o != &q && o.registered && o.p == p) return;
+    hipPointerAttribute_t attr{};
+    if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost) return;
+    (void)hipGetLastError();
+    q.registered = hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) == hipSuccess;
+    (void)hipGetLastError();  // a refused registration leaves the copy pageable, not an error
+}
+
 static int prepare_common(mas_handle h, const float* d_diag9, const float* d_off9, const int* d_ranges, const void* ef,
                           const void* ee, const void* vf, const unsigned* efC, const unsigned* eeC,
                           const unsigned* vfC, hipStream_t s) {
@@ -307,6 +333,9 @@ int mas_prepare(mas_handle h, const float* diag9, const float* off9, const int* 
     MAS_TRY(ensure(h, h->diagStage, nV * 36));
     MAS_TRY(ensure(h, h->offStage, nnz * 36));
     MAS_TRY(ensure(h, h->rangeStage, (nV + 1) * 4));
+    pin_host(h, 0, diag9, nV * 36);
+    pin_host(h, 1, off9, nnz * 36);
+    pin_host(h, 2, ranges, (nV + 1) * 4);
     MAS_TRY(hip_check(h, hipMemcpyAsync(h->diagStage.p, diag9, nV * 36, hipMemcpyHostToDevice, h->stream), "H2D diag"));
     MAS_TRY(hip_check(h, hipMemcpyAsync(h->offStage.p, off9, nnz * 36, hipMemcpyHostToDevice, h->stream), "H2D off"));
     MAS_TRY(hip_check(h, hipMemcpyAsync(h->rangeStage.p, ranges, (nV + 1) * 4, hipMemcpyHostToDevice, h->stream),
@@ -367,6 +396,11 @@ int mas_pcg_solve(mas_handle h, const float* diag9, const float* off9, const int
     MAS_TRY(ensure(h, h->offStage, nnz * 36));
     MAS_TRY(ensure(h, h->rangeStage, (nV + 1) * 4));
     MAS_TRY(ensure(h, h->pcgStage, 2 * vb));
+    pin_host(h, 0, diag9, nV * 36);
+    pin_host(h, 1, off9, nnz * 36);
+    pin_host(h, 2, ranges, (nV + 1) * 4);
+    pin_host(h, 5, x4, vb);
+    pin_host(h, 6, b4, vb);
     float* dx = P<float>(h->pcgStage);
     float* db = dx + 4 * nV;
     MAS_TRY(hip_check(h, hipMemcpyAsync(h->diagStage.p, diag9, nV * 36, hipMemcpyHostToDevice, h->stream), "H2D diag"));
@@ -390,6 +424,8 @@ int mas_apply(mas_handle h, float* z4, const float* r4) {
     const size_t bytes = (size_t)h->nV * 16;
     MAS_TRY(ensure(h, h->rStage, bytes));
     MAS_TRY(ensure(h, h->zStage, bytes));
+    pin_host(h, 3, r4, bytes);
+    pin_host(h, 4, z4, bytes);
     MAS_TRY(hip_check(h, hipMemcpyAsync(h->rStage.p, r4, bytes, hipMemcpyHostToDevice, h->stream), "H2D r"));
     MAS_TRY(run_apply(h, P<float4>(h->zStage), P<float4>(h->rStage), h->stream));
     MAS_TRY(hip_check(h, hipMemcpyAsync(z4, h->zStage.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H z"));
@@ -417,6 +453,8 @@ int mas_profile_fine(mas_handle h, float* d_z4, const float* d_r4, int n, void* 
     if (!h) return MAS_ERR_ARG;
     if (!d_z4 || !d_r4 || !ms_per_launch || n <= 0) return fail(h, MAS_ERR_ARG, "mas_profile_fine: bad arguments");
     if (!h->prepared) return fail(h, MAS_ERR_STATE, "profile before prepare");
+    if ((reinterpret_cast<uintptr_t>(d_z4) | reinterpret_cast<uintptr_t>(d_r4)) & 15)
+        return fail(h, MAS_ERR_ARG, "mas_profile_fine: vectors must be 16-byte aligned");
     if (h->fineBlk0 != 0 || h->fineBlk1 != h->nFineBlk)
         return fail(h, MAS_ERR_STATE, "mas_profile_fine: the handle was prepared for one shard");
     hipSetDevice(h->device);
@@ -552,6 +590,21 @@ int mas_get_neighbors(mas_handle h, int* nbr_num, int* nbr) {
     return MAS_OK;
 }
 
+// a coarse block of a Prepare with the coarse split exists only where the
+// rank factored it (its pre / post ranges, coarse_split.hip), post blocks only
+// after the exchange
+static int coarse_block_ready(mas_handle h, int blk) {
+    if (!h->splitPlanned || blk < h->nFineBlk) return MAS_OK;
+    for (size_t i = 0; i + 1 < h->splitPre.size(); i += 2)
+        if (blk >= h->splitPre[i] && blk < h->splitPre[i + 1]) return MAS_OK;
+    for (size_t i = 0; i + 1 < h->splitPost.size(); i += 2)
+        if (blk >= h->splitPost[i] && blk < h->splitPost[i + 1])
+            return h->rowsPending ? fail(h, MAS_ERR_STATE, "coarse block of a sharded Prepare before the exchange "
+                                                           "(mas_prepare_shard_complete)")
+                                  : MAS_OK;
+    return fail(h, MAS_ERR_STATE, "coarse block another rank of this sharded Prepare assembles");
+}
+
 int mas_get_block_matrix(mas_handle h, int blk, float* out96) {
     if (!h || !out96) return MAS_ERR_ARG;
     if (!h->prepared || h->fromBlob || !h->dense.p)
@@ -559,6 +612,7 @@ int mas_get_block_matrix(mas_handle h, int blk, float* out96) {
     if (blk < 0 || blk >= h->nBlk) return fail(h, MAS_ERR_ARG, "block index out of range");
     if (blk < h->nFineBlk && (blk < h->fineBlk0 || blk >= h->fineBlk1))
         return fail(h, MAS_ERR_STATE, "level-0 block outside the shard this handle was prepared for");
+    MAS_TRY(coarse_block_ready(h, blk));
     if (blk < h->nFineBlk && !h->denseFine)
         return fail(h, MAS_ERR_STATE, "level-0 blocks are not stored by the fused assemble + factor "
                                       "(create the handle with mas_config.keep_blocks = 1)");
@@ -581,9 +635,25 @@ int mas_get_block_inverse(mas_handle h, int blk, float* out96) {
     if (blk < 0 || blk >= h->nBlk) return fail(h, MAS_ERR_ARG, "block index out of range");
     if (blk < h->nFineBlk && (blk < h->fineBlk0 || blk >= h->fineBlk1))
         return fail(h, MAS_ERR_STATE, "level-0 block outside the shard this handle was prepared for");
+    MAS_TRY(coarse_block_ready(h, blk));
     hipSetDevice(h->device);
     hipStreamSynchronize(h->stream);
     return copy_block_inverse(h, blk, out96);
+}
+
+int mas_get_packed_inverses(mas_handle h, int blk0, int nblk, float* out) {
+    if (!h || !out || nblk < 0) return MAS_ERR_ARG;
+    if (!h->prepared) return fail(h, MAS_ERR_STATE, "inverses before prepare");
+    if (blk0 < 0 || blk0 + nblk > h->nBlk) return fail(h, MAS_ERR_ARG, "block range out of range");
+    for (int b = blk0; b < blk0 + nblk; ++b) {
+        if (b < h->nFineBlk && (b < h->fineBlk0 || b >= h->fineBlk1))
+            return fail(h, MAS_ERR_STATE, "level-0 block outside the shard this handle was prepared for");
+        MAS_TRY(coarse_block_ready(h, b));
+    }
+    hipSetDevice(h->device);
+    hipStreamSynchronize(h->stream);
+    return hip_check(h, hipMemcpy(out, P<float>(h->inv) + (size_t)blk0 * kBlockFloats,
+                                  (size_t)nblk * kBlockFloats * 4, hipMemcpyDeviceToHost), "D2H inverses");
 }
 
 int mas_get_coarse_residual(mas_handle h, float* out4) {

@@ -78,6 +78,26 @@ struct FineAsm {
     float* keep;                      // dense base: also store the assembled blocks (null: not kept)
 };
 
+// The node rows a sharded Prepare assembles (coarse_split.hip): level l owns
+// the global ids [lo[l], hi[l]) (level 0: sorted vertices); level l's ids
+// start at begin[l] (begin[l] = INT_MAX for l >= L).  Unsharded: everything.
+struct OwnNodes {
+    int lo[5], hi[5];
+    int begin[5];
+    __host__ __device__ bool own(unsigned x) const {
+        int l = 0;
+#pragma unroll
+        for (int k = 1; k < 5; ++k) l += (long long)x >= (long long)begin[k];
+        return (int)x >= lo[l] && (int)x < hi[l];
+    }
+};
+
+// A run of consecutive node rows of the coarse exchange: rows [node0, node0 +
+// count) of the dense blocks at rows [seg0, seg0 + count) of a segment.
+struct RowPart {
+    int node0, count, seg0;
+};
+
 struct Buffer {
     void* p = nullptr;
     size_t bytes = 0;
@@ -210,6 +230,29 @@ struct mas_context {
     // factors only the level-0 blocks of Morton shard prepRank / prepWorld;
     // [fineBlk0, fineBlk1) = the level-0 blocks the last Prepare factored
     int prepRank = 0, prepWorld = 1, fineBlk0 = 0, fineBlk1 = 0;
+    // Sharded coarse assembly (coarse_split.hip): a
+    // sharded Prepare assembles only the coarse rows whose subtree lies in its
+    // vertex range (own), factors its level-1 blocks no other rank has rows in
+    // (pre), exchanges the rows the other ranks need (its rows of level-1
+    // blocks shared with a neighbour, every level >= 2 row it owns: parts) and
+    // factors the shared level-1 blocks and every level >= 2 block after the
+    // exchange (post).  When the equal split cuts a coarse row's subtree the
+    // rank assembles every row (splitClean false, same exchange).
+    bool splitPlanned = false;   // this Prepare exchanges coarse rows (sharded, L >= 2, fused factor)
+    bool splitClean = false;     // ... and assembles only its own rows
+    mas::OwnNodes own{};         // the rows this Prepare assembles
+    unsigned long long splitHierId = ~0ull;  // the hierarchy / shard the plan below was made for
+    int splitRank = -1, splitWorld = 0;
+    std::vector<int> splitBnd;   // this rank's row range per level l: [splitBnd[2l], splitBnd[2l + 1])
+    std::vector<std::vector<mas::RowPart>> splitParts;  // per rank: its rows in the exchange segment
+    int splitSegRows = 0;        // rows per (padded) segment: the largest rank's
+    std::vector<int> splitPre, splitPost;  // [begin, end) block ranges factored before / after the exchange
+    int splitPackParts = 0, splitPackRows = 0, splitUnpackParts = 0, splitUnpackRows = 0;  // part table (splitPartsDev)
+    bool rowsPending = false;    // the exchange of this Prepare has not run yet (mas_prepare_shard_complete)
+    int odV0 = 0, odV1 = 0;      // the vertex range the early path's od covered (run_level0_early)
+    long long recShardKey = 0;   // the shard the cached coarse records were built for (0: every row)
+    mas_allgather_fn prepAllgather = nullptr;  // mas_set_prepare_allgather: the exchange inside Prepare
+    void* prepAllgatherUser = nullptr;
     int levelSize[2 * 9] = {};
 
     // allocate-phase device data
@@ -265,6 +308,7 @@ struct mas_context {
     mas::Buffer caCnt, caOff, caKeys, caKeysS, caIds, caIdsS, caVal;
     mas::Buffer cpCnt, cpOff, cpKeys, cpKeysS, cpIds, cpIdsS;
     mas::Buffer Rc, Zc, members, coarseMask, shardOff, shardPos1, l1src;
+    mas::Buffer splitDev, prepSeg, prepGathered, splitPartsDev;  // coarse split: bounds + flag, segments, part table
     // Incremental level maps (DESIGN.md section 4 "Prepare").
     // The contact-free ("mesh") hierarchy of the current sort is built once and
     // kept; each Prepare checks on the device whether its contact stencils
@@ -333,6 +377,7 @@ struct mas_context {
     // the communication stream and its fork/join events
     mas::Buffer shardSeg, shardGathered;
     hipStream_t commStream = nullptr;
+    int shardCoarseSide = 1;  // the sharded apply's coarse levels on commStream (env MAS_SHARD_COARSE_SIDE=0: on the apply stream)
     hipEvent_t evRestrict = nullptr, evGathered = nullptr;
     // end of the previous mas_shard_apply_device call and the stream it ran
     // on: a call on another stream waits for it (the segments are the handle's)
@@ -346,6 +391,17 @@ struct mas_context {
     int rbSeq = 0;
     // staging for host-pointer entry points
     mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
+    // The caller's host arrays of the host-pointer entry points, page-locked
+    // (hipHostRegister) on first use so their copies run at the pinned rate:
+    // one slot per argument, kept while the same (pointer, size) comes back,
+    // released when another array is passed there and by mas_destroy (env
+    // MAS_HOST_REGISTER=0: never).  Slots: diag, off, ranges, r, z, pcg x, pcg b.
+    struct HostPin {
+        const void* p = nullptr;
+        size_t bytes = 0;
+        bool registered = false;
+    } pins[7];
+    int hostRegister = 1;
     // hipcub scratch
     mas::Buffer cubTemp;
     // look-back-free radix sort and scan (rsort.hip): ping-pong keys/values,
@@ -373,7 +429,7 @@ struct mas_context {
                               &tab, &termCnt,
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cdEnt, &c0Ent, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
-                              &cpIdsS, &Rc, &Zc, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &cpIdsS, &Rc, &Zc, &splitDev, &prepSeg, &prepGathered, &splitPartsDev, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart, &rsKeysP, &rsValsP, &rsHistP, &rsPartP, &add0, &c0Cnt, &c0Off, &c0Keys, &c0KeysS, &c0Ids, &c0IdsS,
                               &c0Val, &a0Keys, &a0KeysS, &a0Ids, &a0IdsS, &a0Val,
                               &spCst, &spGn, &spVmap, &spCoarseTables, &spFine, &spCoarseMask, &hierFlags, &recRanges,
@@ -434,6 +490,15 @@ bool early_od(const mas_context* h);  // od and the record counts computed by th
 int early_buffers(mas_context* h);    // the early path's buffers the caller reads too (run_prepare sizes them)
 int prep_stream_init(mas_context* h);  // prepStream (CU-masked) and its events
 int run_factor(mas_context* h, hipStream_t s);
+// factor blocks [b0, b1) in the coarse form (identity fix + k_factor_rb / k_factor) (k_factor.hip)
+int factor_blocks(mas_context* h, int b0, int b1, hipStream_t s);
+// coarse_split.hip: the split plan of a sharded Prepare (after the level build),
+// the pack of this rank's rows, the exchange's second half (unpack + factor)
+int plan_coarse_split(mas_context* h, hipStream_t s);
+int pack_coarse_rows(mas_context* h, hipStream_t s);
+int complete_coarse_rows(mas_context* h, const float* gathered, hipStream_t s);
+// the Prepare status words (pivot checks): stats + the non-SPD warning / error (prepare.hip)
+int report_pivots(mas_context* h, hipStream_t s);
 // fused level-0 assemble + factor of blocks [blk0, blk1) (k_factor.hip)
 int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s);
 int run_apply(mas_context* h, float4* d_z, const float4* d_r, hipStream_t s);
@@ -478,6 +543,8 @@ int pending_giveup(mas_context* h);
 int read_back_post(mas_context* h, hipStream_t s, std::initializer_list<const int*> src, int* seq);
 int read_back_wait(mas_context* h, hipStream_t s, int seq, int* out, int n);
 void release_comm(mas_context* h);  // comm_rccl.hip
+// an allgather of `bytes` per rank over the handle's RCCL communicator on s (comm_rccl.hip)
+int comm_allgather(mas_context* h, const void* send, void* recv, size_t bytes, hipStream_t s);
 int copy_block_inverse(mas_context* h, int blk, float* out96);
 int run_pcg(mas_context* h, const float* d_diag9, const float* d_off9, const int* d_ranges, float4* d_x,
             const float4* d_b, int maxIters, float tol, int precondition, mas_pcg_result* res, hipStream_t s);

@@ -93,15 +93,37 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     }
     if (h->fusedAfterLevels && ((rc = finish_early(h)) || (h->earlyFused && (rc = launch_level0_fused(h, s)))))
         return rc;
+    // a sharded Prepare: which coarse rows this rank assembles (coarse_split.hip)
+    if ((rc = plan_coarse_split(h, s))) return rc;
     hipEventRecord(e0, s);
     if ((rc = run_assemble(h, d_diag9, d_off9, d_ranges, s)) || (rc = finish_early(h))) return rc;
     hipEventRecord(e1, s);
     if ((rc = run_factor(h, s))) return rc;
+    // the coarse rows other ranks need; exchanged here when the handle has a
+    // communicator of this shard or an allgather hook, else by the caller
+    // (mas_prepare_shard_rows / mas_prepare_shard_complete)
+    if (h->splitPlanned) {
+        if ((rc = pack_coarse_rows(h, s))) return rc;
+        const bool viaRccl = h->rcclComm && h->rcclRank == h->prepRank && h->rcclWorld == h->prepWorld;
+        if (viaRccl || h->prepAllgather) {
+            const size_t segBytes = (size_t)h->splitSegRows * 1152;
+            if ((rc = ensure(h, h->prepGathered, segBytes * h->prepWorld))) return rc;
+            if (viaRccl) {
+                if ((rc = comm_allgather(h, h->prepSeg.p, h->prepGathered.p, segBytes, s))) return rc;
+            } else if (int e = h->prepAllgather(h->prepSeg.p, h->prepGathered.p, segBytes, s, h->prepAllgatherUser)) {
+                return fail(h, MAS_ERR_COMM, "Prepare's allgather hook returned " + std::to_string(e));
+            }
+            if ((rc = complete_coarse_rows(h, P<float>(h->prepGathered), s))) return rc;
+        }
+    }
     const int nCoarseNodes = h->totalClusters - h->levelSize[3];
     if ((rc = ensure(h, h->Rc, (size_t)(nCoarseNodes > 0 ? nCoarseNodes : 1) * 16)) ||
         (rc = ensure(h, h->Zc, (size_t)(nCoarseNodes > 0 ? nCoarseNodes : 1) * 16)))
         return rc;
-    if (nCoarseNodes > 0 && (rc = hip_check(h, hipMemsetAsync(h->Rc.p, 0, (size_t)nCoarseNodes * 16, s), "memset Rc")))
+    // Zc too: mas_profile_fine prolongs from it before the first apply has written it
+    if (nCoarseNodes > 0 &&
+        ((rc = hip_check(h, hipMemsetAsync(h->Rc.p, 0, (size_t)nCoarseNodes * 16, s), "memset Rc")) ||
+         (rc = hip_check(h, hipMemsetAsync(h->Zc.p, 0, (size_t)nCoarseNodes * 16, s), "memset Zc"))))
         return rc;
     // the apply tables depend on the hierarchy alone: kept while it is unchanged
     if (!h->hierCache || h->tabHierId != h->hierId) {
@@ -136,10 +158,17 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     h->stats.factor_formation = (h->factorVariant == 5 || h->factorVariant == 3) ? 1 : 0;
     h->stats.hier_dirty_level = h->hierCache ? h->lastHierDirty : -1;
     h->stats.hier_rebuilt = h->lastHierBuilt ? 1 : 0;
+    h->stats.coarse_split = h->splitPlanned ? (h->splitClean ? 1 : 2) : 0;
+    h->prepared = true;  // as the reference: the inverses exist (with the bad pivots in them)
+    return report_pivots(h, s);
+}
+
+int report_pivots(mas_context* h, hipStream_t s) {
+    int* status = P<int>(h->devStatus);
     int bad[2] = {0, 0};
+    int rc;
     if ((rc = read_back(h, s, {status, status + 1}, bad))) return rc;
     h->stats.nonspd_blocks = bad[0];
-    h->prepared = true;  // as the reference: the inverses exist (with the bad pivots in them)
     if (bad[0] > 0) {
         int level = 0;
         for (int l = 1; l < h->L; ++l)

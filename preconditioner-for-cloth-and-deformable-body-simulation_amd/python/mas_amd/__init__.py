@@ -39,9 +39,12 @@ EXPORTS = ["mas_version", "mas_create", "mas_destroy", "mas_last_error", "mas_al
            "mas_prepare_device", "mas_apply", "mas_apply_device", "mas_set_profiling", "mas_profile_fine",
            "mas_profile_coarse", "mas_get_info",
            "mas_get_stats", "mas_get_maps", "mas_get_neighbors", "mas_get_block_matrix", "mas_get_block_inverse",
-           "mas_get_coarse_residual", "mas_set_prepare_shard",
+           "mas_get_packed_inverses",
+           "mas_get_coarse_residual", "mas_set_prepare_shard", "mas_set_prepare_allgather", "mas_prepare_shard_rows",
+           "mas_prepare_shard_complete",
            "mas_shard_plan", "mas_shard_setup", "mas_apply_shard_restrict", "mas_apply_shard_finish",
-           "mas_apply_shard_fine", "mas_apply_shard_complete", "mas_shard_apply_device", "mas_rccl_unique_id",
+           "mas_apply_shard_fine", "mas_apply_shard_complete", "mas_shard_apply_device", "mas_allgather_loopback",
+           "mas_rccl_unique_id",
            "mas_rccl_init", "mas_shard_apply_rccl",
            "mas_pcg_solve_device", "mas_pcg_solve", "mas_blob_size", "mas_save_blob", "mas_load_blob",
            "mas_blob_validate", "mas_dev_sort_pairs", "mas_dev_exclusive_scan", "mas_dev_contact_terms"]
@@ -70,7 +73,9 @@ class mas_stats(ctypes.Structure):
                [("apply_mode", ctypes.c_int64), ("prepare_fine_ms", ctypes.c_double),
                 ("factor_formation", ctypes.c_int64), ("hier_dirty_level", ctypes.c_int64),
                 ("hier_rebuilt", ctypes.c_int64), ("prepare_fine_start_ms", ctypes.c_double),
-                ("nonspd_blocks", ctypes.c_int64), ("wait_timeouts", ctypes.c_int64), ("reserved", ctypes.c_int64 * 3)]
+                ("nonspd_blocks", ctypes.c_int64), ("wait_timeouts", ctypes.c_int64),
+                ("prepare_complete_ms", ctypes.c_double), ("coarse_split", ctypes.c_int64),
+                ("reserved", ctypes.c_int64 * 1)]
 
 
 class mas_shard(ctypes.Structure):
@@ -136,8 +141,12 @@ def lib():
         L.mas_get_neighbors.argtypes = [P, P, P]
         L.mas_get_block_matrix.argtypes = [P, I, P]
         L.mas_get_block_inverse.argtypes = [P, I, P]
+        L.mas_get_packed_inverses.argtypes = [P, I, I, P]
         L.mas_get_coarse_residual.argtypes = [P, P]
         L.mas_set_prepare_shard.argtypes = [P, I, I]
+        L.mas_set_prepare_allgather.argtypes = [P, ALLGATHER_FN, P]
+        L.mas_prepare_shard_rows.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+        L.mas_prepare_shard_complete.argtypes = [P, P, P]
         L.mas_shard_plan.argtypes = [I, P, I, I, ctypes.POINTER(mas_shard)]
         L.mas_shard_setup.argtypes = [P, I, I, ctypes.POINTER(mas_shard)]
         L.mas_apply_shard_restrict.argtypes = [P, I, I, P, P, P]
@@ -233,6 +242,8 @@ class SeSchwarzPreconditioner:
         self._nnz = 0
         self._allocated = False   # Allocate inputs present (a restored blob has none)
         self._plans = {}
+        self._rows_pending = False  # a sharded Prepare's coarse-row exchange has not run yet
+        self._shard_world = 1
 
     def __del__(self):
         try:
@@ -294,6 +305,7 @@ class SeSchwarzPreconditioner:
         self._check(self._L.mas_prepare(self.h, _ptr(d), _ptr(o), _ptr(r), _ptr(efSets), _ptr(eeSets), _ptr(vfSets),
                                         _ptr(efC), _ptr(eeC), _ptr(vfC)), "PreparePreconditioner")
         self._warn_prepare("PreparePreconditioner")
+        self._rows_pending = self._shard_world > 1 and self.prepare_shard_rows() is not None
 
     def PreparePreconditionerDevice(self, d_diag, d_off, d_ranges, efSets=None, eeSets=None, vfSets=None,
                                     efCounts=None, eeCounts=None, vfCounts=None, stream=None):
@@ -310,6 +322,7 @@ class SeSchwarzPreconditioner:
                                                _ptr(eeSets), _ptr(vfSets), _ptr(efC), _ptr(eeC), _ptr(vfC),
                                                _ptr(stream)), "PreparePreconditionerDevice")
         self._warn_prepare("PreparePreconditionerDevice")
+        self._rows_pending = self._shard_world > 1 and self.prepare_shard_rows() is not None
 
     def Preconditioning(self, z, residual, dim=None):
         self._need("Preconditioning")
@@ -331,6 +344,29 @@ class SeSchwarzPreconditioner:
         z = _dev(z, self._nV, 4, "float32", "z")
         residual = _dev(residual, self._nV, 4, "float32", "residual")
         self._check(self._L.mas_apply_device(self.h, _ptr(z), _ptr(residual), _ptr(stream)), "PreconditioningDevice")
+
+    # ---- the sharded coarse assembly (include/mas_capi.h, ABI 5) ----
+    def prepare_shard_rows(self):
+        """(device pointer, bytes) of this rank's coarse-row segment after a
+        sharded Prepare, or None when no exchange is pending."""
+        ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
+        rc = self._L.mas_prepare_shard_rows(self.h, ctypes.byref(ptr), ctypes.byref(n))
+        if rc == -4:  # MAS_ERR_STATE: nothing pending
+            return None
+        self._check(rc, "prepare_shard_rows")
+        return int(ptr.value), int(n.value)
+
+    def prepare_shard_complete(self, gathered, stream=None):
+        """Unpack the allgathered segments ([world][bytes], device) and factor
+        the blocks that needed them (synchronous)."""
+        self._check(self._L.mas_prepare_shard_complete(self.h, _ptr(gathered), _ptr(stream)),
+                    "prepare_shard_complete")
+        self._rows_pending = False
+        self._warn_prepare("prepare_shard_complete")
+
+    @property
+    def rows_pending(self) -> bool:
+        return self._rows_pending
 
     # ---- Morton-range sharding (include/mas_capi.h) ----
     def shard_setup(self, rank, world) -> dict:
@@ -392,6 +428,17 @@ class SeSchwarzPreconditioner:
         if err:
             raise MasError(f"shard_apply: allgather hook failed: {err[0]!r}") from err[0]
         self._check(rc, "shard_apply")
+
+    def shard_apply_loopback(self, rank, world, z, r, stream=None):
+        """mas_shard_apply_device with the library's one-process stand-in for
+        the collective (mas_allgather_loopback: only this rank's slot of the
+        gathered buffer is written): per-rank timing / tests on one GPU."""
+        v = self._shard_vecs(rank, world, r=r, z=z)
+        r, z = v["r"], v["z"]
+        fn = ALLGATHER_FN(ctypes.cast(self._L.mas_allgather_loopback, ctypes.c_void_p).value)
+        rk = ctypes.c_int(rank)
+        self._check(self._L.mas_shard_apply_device(self.h, rank, world, fn, ctypes.cast(ctypes.pointer(rk), ctypes.c_void_p), _ptr(z), _ptr(r),
+                                                   _ptr(stream)), "shard_apply_loopback")
 
     def rccl_init(self, unique_id: bytes, rank, world):
         """Give the handle its own RCCL communicator (mas_rccl_init)."""
@@ -519,6 +566,13 @@ class SeSchwarzPreconditioner:
     def set_prepare_shard(self, rank: int, world: int):
         """Later Prepares factor only the level-0 blocks of shard rank/world (mas_set_prepare_shard)."""
         self._check(self._L.mas_set_prepare_shard(self.h, int(rank), int(world)), "set_prepare_shard")
+        self._shard_world = int(world)
+
+    def packed_inverses(self, blk0: int, nblk: int) -> np.ndarray:
+        """Blocks [blk0, blk0 + nblk)'s inverses as stored, [nblk, 4656] float32."""
+        out = np.empty((nblk, 4656), np.float32)
+        self._check(self._L.mas_get_packed_inverses(self.h, int(blk0), int(nblk), _ptr(out)), "packed_inverses")
+        return out
 
     def coarse_residual(self):
         """R of every coarse node (ids begin_1 .. total_clusters-1) after the last apply, [n, 4] float32."""
@@ -548,6 +602,30 @@ def from_mesh(mesh, max_levels=0, contacts=None, shard=None, **kw) -> SeSchwarzP
         vf, vfC = contacts
         P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, vf, None, None, vfC)
     return P
+
+
+def exchange_coarse_rows(handles, stream=None):
+    """The coarse-row exchange of a world of shard-prepared handles that all
+    live in this process (virtual shards on one GPU, tests and per-rank
+    timing): the ranks' segments concatenated in rank order, as an allgather
+    delivers them, then prepare_shard_complete on every handle.  Returns the
+    gathered buffer (a torch uint8 cuda tensor)."""
+    import torch
+    from .distributed import device_view
+    segs = [P.prepare_shard_rows() for P in handles]
+    if any(sg is None for sg in segs):
+        raise MasError("exchange_coarse_rows: a handle has no coarse rows pending")
+    nbytes = segs[0][1]
+    if any(sg[1] != nbytes for sg in segs):
+        raise MasError("exchange_coarse_rows: the handles' segment sizes differ (not one world)")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    gathered = torch.empty(len(handles) * nbytes // 4, dtype=torch.float32, device=dev)
+    for g, (ptr, _) in enumerate(segs):
+        gathered[g * nbytes // 4:(g + 1) * nbytes // 4].copy_(device_view(ptr, nbytes // 4, dev))
+    torch.cuda.synchronize()
+    for P in handles:
+        P.prepare_shard_complete(gathered, stream)
+    return gathered
 
 
 def rccl_unique_id() -> bytes:

@@ -38,6 +38,33 @@ def device_view(ptr: int, n: int, device) -> torch.Tensor:
     return torch.as_tensor(_DeviceArray(ptr, n), device=device)
 
 
+def exchange_coarse_rows(P, group=None, device=None) -> bool:
+    """The second half of a sharded Prepare (include/mas_capi.h ABI 5): one
+    allgather of every rank's coarse-row segment over `group` (nccl = RCCL;
+    gloo stages through the host), then mas_prepare_shard_complete.  Every
+    rank calls it after its Prepare; returns False when nothing was pending
+    (unsharded, or the exchange ran inside Prepare over the handle's RCCL
+    communicator)."""
+    seg = P.prepare_shard_rows() if P.rows_pending else None
+    if seg is None:
+        return False
+    ptr, nbytes = seg
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    world = dist.get_world_size(group)
+    n = nbytes // 4
+    src = device_view(ptr, n, dev)
+    if dist.get_backend(group) == "gloo":
+        torch.cuda.synchronize(dev)
+        g = torch.empty(n * world, dtype=torch.float32)
+        dist.all_gather_into_tensor(g, src.cpu(), group=group)
+        gathered = g.to(dev)
+    else:
+        gathered = torch.empty(n * world, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(gathered, src, group=group)
+    P.prepare_shard_complete(gathered, torch.cuda.current_stream(dev).cuda_stream)
+    return True
+
+
 class ShardedApply:
     def __init__(self, P, rank: int, world: int, group=None, device=None, overlap=None, transport="torch"):
         self.P, self.rank, self.world, self.group = P, rank, world, group
@@ -78,6 +105,8 @@ class ShardedApply:
                 dist.all_gather_into_tensor(dst, src, group=self.group)
 
     def _call(self, z, r, s):
+        if self.P.rows_pending:  # the first apply after a sharded Prepare: its coarse-row exchange first
+            exchange_coarse_rows(self.P, self.group, self.device)
         if self.transport == "rccl":
             self.P.shard_apply_rccl(z, r, s.cuda_stream)
         else:

@@ -1,6 +1,8 @@
 """Per-rank compute of the Morton-range sharded apply, measured on ONE GPU:
 rank g of a world of W runs restrict -> (allgather replaced by a device copy
-of its own segment; the communication is NOT in these numbers) -> finish.
+of its own segment; the communication is NOT in these numbers) -> finish;
+mode one_call: mas_shard_apply_device with the loopback stand-in
+(mas_allgather_loopback), the coarse levels on the communication stream.
 Prints ms per apply for every (W, g) so the critical path of an N-GPU apply
 can be read as max_g(compute) + allgather.  Dev tool; GPU only."""
 import json
@@ -24,7 +26,8 @@ z = torch.zeros_like(r)
 s = torch.cuda.Stream()
 out = {}
 steps = 200
-for W, overlap in [(w, o) for w in worlds for o in (False, True)]:
+modes = (sys.argv[3] if len(sys.argv) > 3 else "finish,fine_then_complete,one_call").split(",")
+for W, mode in [(w, m) for w in worlds for m in modes]:
     for g in sorted({0, W - 1}):
         plan = P.shard_setup(g, W)
         seg = torch.zeros((plan["seg_max"], 4), dtype=torch.float32, device="cuda")
@@ -32,10 +35,13 @@ for W, overlap in [(w, o) for w in worlds for o in (False, True)]:
         dst = gathered[g * plan["seg_max"]:(g + 1) * plan["seg_max"]]
 
         def step():
+            if mode == "one_call":  # mas_shard_apply_device: coarse levels on the comm stream (round 6)
+                P.shard_apply_loopback(g, W, z, r, s.cuda_stream)
+                return
             P.shard_restrict(g, W, r, seg, s.cuda_stream)
             with torch.cuda.stream(s):
                 dst.copy_(seg)
-            if overlap:
+            if mode == "fine_then_complete":
                 P.shard_fine(g, W, r, z, s.cuda_stream)
                 P.shard_complete(g, W, gathered, z, s.cuda_stream)
             else:
@@ -57,7 +63,7 @@ for W, overlap in [(w, o) for w in worlds for o in (False, True)]:
         torch.cuda.synchronize()
         st = P.stats()
         P.set_profiling(False)
-        key = f"W{W}/rank{g}/" + ("fine_then_complete" if overlap else "finish")
+        key = f"W{W}/rank{g}/{mode}"
         out[key] = {"ms_per_apply": round(ms, 5), "pre_fine_ms": round(st["pre_fine_ms_avg"], 5),
                                 "fine_ms": round(st["fine_ms_avg"], 5), "post_fine_ms": round(st["post_fine_ms_avg"], 5),
                                 "fine_blocks": plan["fine_block_end"] - plan["fine_block_begin"]}

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(mas_amd.LIB_PATH)
     missing = [s for s in _declared("mas_capi.h") if not hasattr(lib, s)]
     assert not missing, missing
-    assert lib.mas_version() == 4
+    assert lib.mas_version() == 5
 
 
 def test_facade_exports_reference_methods():

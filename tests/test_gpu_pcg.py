@@ -131,12 +131,13 @@ def test_pcg_edge_cases():
 
 
 @pytest.mark.parametrize("W,L,precondition,maxit", [(100, 3, True, 3000), (256, 4, True, 3000), (100, 3, False, 3000),
-                                                    (100, 3, True, 7)])
+                                                    (100, 3, True, 7), (101, 3, True, 3000), (101, 3, False, 3000)])
 def test_pcg_fused_p_update_bitwise(W, L, precondition, maxit, monkeypatch):
     """p = z + beta p inside the next SpMV (MAS_PCG_FUSE_P=1, the default) and
     as its own pass (0): the same iterates bit for bit -- x, the iteration
     counts, the replacements, the residuals -- also when max_iters stops the
-    solve (the last decision then runs after the loop)."""
+    solve (the last decision then runs after the loop).  W = 101: an odd
+    vertex count (the second p buffer's offset must stay 16-byte aligned)."""
     import mas_amd
     from mas_amd import meshgen
     mesh = cloth(W)

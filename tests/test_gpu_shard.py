@@ -94,9 +94,33 @@ def test_shard_prepared_handles_bitwise(kind, W, L, world, nc):
     z_ref = _unsharded(Pf, r)
     t_full = Pf.stats()["prepare_fine_ms"]
     ranks = [mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, shard=(g, world)) for g in range(world)]
+    mas_amd.exchange_coarse_rows(ranks)
     s = torch.cuda.Stream()
     plans = [Pg.shard_setup(g, world) for g, Pg in enumerate(ranks)]
     seg = plans[0]["seg_max"]
+    # the coarse blocks a rank's sharded apply reads -- its level-1 blocks
+    # and every level >= 2 block -- bitwise the unsharded Prepare's, from
+    # the rows it assembled itself plus the exchanged ones (coarse_split.hip)
+    info = Pf.info()
+    ls, nblk, nl = info["level_size"], info["num_blocks"], info["num_levels"]
+    b1 = int(ls[1][1]) // 32
+    # cloth-100 / 3 ranks: the equal split cuts level-2 subtrees (every rank
+    # assembles every row, mode 2); the others are clean (own rows, mode 1)
+    want_mode = 2 if (kind, W, world) == ("cloth", 100, 3) else 1
+    for g, Pg in enumerate(ranks):
+        assert Pg.stats()["coarse_split"] == want_mode, (g, Pg.stats()["coarse_split"])
+        pl = plans[g]
+        ranges = [(b1 + pl["l1_begin"] // 32, b1 + (pl["l1_end"] + 31) // 32)]
+        if nl > 2:
+            ranges.append((int(ls[2][1]) // 32, nblk))
+        for a, b in ranges:
+            got, want = Pg.packed_inverses(a, b - a), Pf.packed_inverses(a, b - a)
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (g, a, b)
+        for blk in sorted({ranges[0][0], ranges[0][1] - 1} | (set(range(*ranges[1])) if nl > 2 else set())):
+            assert np.array_equal(Pg.block_matrix(blk).view(np.uint32), Pf.block_matrix(blk).view(np.uint32)), (g, blk)
+    if want_mode == 1 and b1 + 1 < ranges[0][0]:  # another rank's level-1 block is not this one's
+        with pytest.raises(mas_amd.MasError, match="STATE"):
+            ranks[-1].packed_inverses(b1, 1)
     with torch.cuda.stream(s):
         segs = [torch.zeros((seg, 4), dtype=torch.float32, device="cuda") for _ in range(world)]
         for g, Pg in enumerate(ranks):
@@ -107,10 +131,13 @@ def test_shard_prepared_handles_bitwise(kind, W, L, world, nc):
             Pg.shard_finish(g, world, gathered, r, z, s.cuda_stream)
     s.synchronize()
     assert torch.equal(z, z_ref), float((z - z_ref).abs().max())
-    # timing is reported, not asserted here (a shared box makes it a flake
-    # source): scripts/dev/prep_shard.py measures the per-rank Prepare
+    # a loose bound only (a shared box makes a tight one a flake source; at
+    # world 8 the rank's level-0 kernel measures ~0.16x the unsharded one):
+    # scripts/dev/prep_shard.py measures the per-rank Prepare
     t_rank = max(Pg.stats()["prepare_fine_ms"] for Pg in ranks)
     print(f"level-0 assemble + factor: unsharded {t_full:.3f} ms, slowest of {world} ranks {t_rank:.3f} ms")
+    if mesh.nV >= 1 << 20:  # small meshes' kernels are one block's latency either way
+        assert t_rank < 0.5 * t_full, (t_rank, t_full)
     P1 = ranks[1]
     with pytest.raises(mas_amd.MasError, match="STATE"):
         P1.PreconditioningDevice(torch.zeros_like(r), r, s.cuda_stream)
@@ -157,21 +184,27 @@ def test_sharded_apply_helper_overlap_world1():
         assert np.array_equal(z.cpu().numpy(), P.Preconditioning(None, r.cpu().numpy())), overlap
 
 
-@pytest.mark.parametrize("kind,W,L,worlds,nc", [("cloth", 100, 3, (1, 2, 3), 0), ("tet", 16, 3, (2, 8), 0),
-                                                ("cloth", 1024, 4, (8,), 100_000)])
-def test_one_call_shard_apply_bitwise(kind, W, L, worlds, nc):
-    """mas_shard_apply_device (the collective inside the library, the level-0
-    solves overlapping it on the apply stream): with an in-process allgather
-    hook -- it writes every rank's segment into `recv` through the step-wise
-    restrict, so all ranks' calls run in one process -- the union of the
-    ranks' own z entries equals the unsharded apply bitwise."""
+@pytest.mark.parametrize("kind,W,L,worlds,nc,refr", [("cloth", 100, 3, (1, 2, 3), 0, False),
+                                                     ("tet", 16, 3, (2, 8), 0, False),
+                                                     ("cloth", 1024, 4, (8,), 100_000, False),
+                                                     ("cloth", 1024, 4, (8,), 100_000, True),
+                                                     ("tet", 160, 4, (8,), 0, False)])
+def test_one_call_shard_apply_bitwise(kind, W, L, worlds, nc, refr):
+    """mas_shard_apply_device (the collective inside the library; the coarse
+    levels on its communication stream right behind the gather, beside the
+    level-0 solves on the apply stream): with an in-process allgather hook --
+    it writes every rank's segment into `recv` through the step-wise restrict,
+    so all ranks' calls run in one process -- the union of the ranks' own z
+    entries equals the unsharded apply bitwise, with the grouped level 3 and
+    the reference's (refr).  World 1 through the loopback stand-in takes the
+    same two-stream path."""
     import torch
     import mas_amd
     from mas_amd import meshgen
     from mas_amd.distributed import device_view
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=3) if nc else None
-    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts)
+    P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, reference_restriction=refr)
     r = torch.from_numpy(meshgen.residual(mesh.nV, 8)).cuda()
     z_ref = _unsharded(P, r)
     s = torch.cuda.Stream()
@@ -191,6 +224,11 @@ def test_one_call_shard_apply_bitwise(kind, W, L, worlds, nc):
         s.synchronize()
         assert torch.equal(z, z_ref), (world, float((z - z_ref).abs().max()))
         assert len(calls) == (world if world > 1 else 0)
+    z1 = torch.full_like(r, float("nan"))
+    for _ in range(2):  # the second call reuses the comm stream and tables
+        P.shard_apply_loopback(0, 1, z1, r, stream=s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(z1, z_ref)
 
 
 def test_one_call_shard_apply_errors():
