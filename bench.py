@@ -191,7 +191,62 @@ def cpu_baseline(mesh, cfg, contacts, r_np, steps):
     return out, z
 
 
-PREP_KEYS = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms", "prepare_fine_ms")
+def host_path(P, mesh, contacts, r_np, make_handle, reps=5, applies=20):
+    """The drop-in host-pointer path (SeSchwarzPreconditioner.h:59-63): a PCG
+    loop that already calls the reference passes host arrays, so Prepare
+    copies the CSR Hessian H2D and every apply copies r in and z out.  Wall
+    time of the synchronous calls, median of `reps` Prepares / `applies`
+    applies after the first (the second call with the same arrays page-locks them,
+    mas_capi.hip pin_host); the same with MAS_HOST_REGISTER=0 (the runtime's
+    pageable staging) on a second handle for comparison."""
+    import numpy as np
+
+    def prep(h):
+        if contacts is None:
+            h.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
+        else:
+            h.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, contacts[0], None, None, contacts[1])
+
+    def measure(h):
+        z_np = np.empty_like(r_np)
+        t = time.perf_counter()
+        prep(h)
+        first = time.perf_counter() - t
+        tp, ta = [], []
+        for _ in range(reps):
+            t = time.perf_counter()
+            prep(h)
+            tp.append(time.perf_counter() - t)
+        dev_ms = h.stats()["prepare_ms"]
+        h.Preconditioning(z_np, r_np)
+        for _ in range(applies):
+            t = time.perf_counter()
+            h.Preconditioning(z_np, r_np)
+            ta.append(time.perf_counter() - t)
+        return {"prepare_ms_incl_h2d": round(statistics.median(tp) * 1e3, 3),
+                "prepare_first_call_ms_incl_h2d": round(first * 1e3, 3),
+                "prepare_ms_device": round(dev_ms, 3),
+                "apply_ms_incl_pcie": round(statistics.median(ta) * 1e3, 4)}, z_np
+
+    nV, nnz = mesh.nV, int(mesh.starts[-1])
+    pinned, z1 = measure(P)
+    os.environ["MAS_HOST_REGISTER"] = "0"
+    try:
+        P2 = make_handle()
+        pageable, z2 = measure(P2)
+        del P2
+    finally:
+        del os.environ["MAS_HOST_REGISTER"]
+    return {**pinned, "pageable": pageable,
+            "z_bitwise_pinned_vs_pageable": bool(np.array_equal(z1.view(np.uint32), z2.view(np.uint32))),
+            "h2d_bytes_prepare": nV * 36 + nnz * 36 + (nV + 1) * 4, "pcie_bytes_apply": 2 * 16 * nV,
+            "note": "host arrays through mas_prepare / mas_apply (synchronous), wall clock; the caller's arrays "
+                    "are page-locked when passed a second time and cached by (pointer, size); value and roofline use "
+                    "device-resident vectors"}
+
+
+PREP_KEYS = ("prepare_ms", "prepare_levels_ms", "prepare_assemble_ms", "prepare_factor_ms", "prepare_fine_ms",
+             "prepare_complete_ms", "prepare_wall_ms")
 
 
 class LaunchError(SystemExit):
@@ -298,6 +353,7 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcg", action="store_true", help="skip the end-to-end PCG solve report")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the host-pointer (PCIe-inclusive) report")
     ap.add_argument("--sharded", action="store_true",
                     help="use the Morton-range sharded apply even on one GPU (overhead measurement)")
     ap.add_argument("--graph", action="store_true",
@@ -369,14 +425,29 @@ def main():
     st_first = P.stats()
     # steady-state Prepare (the per-solve call in a simulator): buffers exist,
     # repeat it and keep the median; the first call also allocates
+    # A sharded Prepare (ABI 5) is mas_prepare (own coarse rows) + one
+    # allgather of the coarse-row segments + mas_prepare_shard_complete; its
+    # prepare_ms here is the two device parts, prepare_wall_ms the host wall
+    # clock of all three (the collective included)
+    from mas_amd.distributed import exchange_coarse_rows
     reps = []
     for _ in range(3):
+        if dist is not None:
+            dist.barrier()
+        t = time.perf_counter()
         if contacts is None:
             P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
         else:
             P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, contacts[0], None, None,
                                     contacts[1])
-        reps.append(P.stats())
+        exchanged = sharded_path and exchange_coarse_rows(P, None, torch.device("cuda", local))
+        wall_ms = (time.perf_counter() - t) * 1e3
+        stp = P.stats()
+        stp["prepare_wall_ms"] = wall_ms
+        stp["prepare_device_only_ms"] = stp["prepare_ms"]
+        if exchanged:
+            stp["prepare_ms"] = stp["prepare_ms"] + stp["prepare_complete_ms"]
+        reps.append(stp)
     st0 = sorted(reps, key=lambda d: d["prepare_ms"])[1]
     seed = 0x5EED + CONFIG_ORDER.index(args.config)
     r_np = meshgen.residual(mesh.nV, seed)
@@ -577,8 +648,10 @@ def main():
         "apply_algorithmic_GBps": round(apply_bytes / (t_max / args.steps) / 1e9, 1),
         "apply_bytes": apply_bytes,
         "prepare_ms": round(st0["prepare_ms"], 3),
-        "prepare_scope": (f"sharded Prepare, slowest of {world} ranks (own level-0 blocks + replicated coarse levels)"
-                          if sharded_path else "whole problem"),
+        "prepare_scope": (f"sharded Prepare, slowest of {world} ranks: own level-0 blocks and own coarse rows "
+                          f"(coarse_split {st0.get('coarse_split')}), + mas_prepare_shard_complete; the coarse-row "
+                          f"allgather is in prepare_wall_ms only" if sharded_path else "whole problem"),
+        "prepare_wall_ms": round(st0["prepare_wall_ms"], 3),
         "prepare_first_call_ms": round(st_first["prepare_ms"], 3),
         "prepare_breakdown_ms": {"levels": round(st0["prepare_levels_ms"], 3),
                                  "assemble": round(st0["prepare_assemble_ms"], 3),
@@ -625,6 +698,13 @@ def main():
             out["pcg_solve"] = pcg
         except Exception as e:  # context only
             log(f"pcg report failed: {e!r}")
+
+    if rank == 0 and world == 1 and not args.no_host_path:
+        try:
+            out["host_path"] = host_path(P, mesh, contacts, r_np, lambda: mas_amd.from_mesh(
+                mesh, max_levels=cfg["levels"], contacts=contacts, device=local))
+        except Exception as e:  # context only
+            log(f"host path report failed: {e!r}")
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

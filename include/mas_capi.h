@@ -313,13 +313,13 @@ int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_g
  * The whole per-rank Preconditioning of a Morton-range shard behind the
  * reference's apply (SeSchwarzPreconditioner.h:63), so a C/C++ simulator that
  * links the library can shard without Python: restrict the own level-1
- * segment, allgather the segments, solve.  The level-0 block solves of the
- * rank run on `stream` while the allgather is in flight on the handle's own
- * communication stream (which first waits for the restrict); the coarse
- * levels and the prolongation follow once it is done.
- * z is written for the rank's own vertices only; the union over ranks is
- * bitwise equal to mas_apply_device.  The segment buffers belong to the
- * handle.
+ * segment, allgather the segments, solve.  By default every step, the
+ * collective included, is enqueued on `stream` (a cross-stream hop costs
+ * more on MI355X than the overlap it would buy; env
+ * MAS_SHARD_MODE=1 / 2 runs the collective on the handle's communication
+ * stream beside the level-0 solves instead).  z is written for the rank's own
+ * vertices only; the union over ranks is bitwise equal to mas_apply_device.
+ * The segment buffers belong to the handle.
  *
  * mas_allgather_fn: enqueue on `stream` (a hipStream_t) an allgather of
  * `bytes` from `send` into `recv` (world x bytes, rank-major) and return 0, or

@@ -750,6 +750,10 @@ __global__ __launch_bounds__(256) void k_records(int nV, int L, RecKey rk, const
 // (Collecting the long runs into a list with a counter was measured first: ~60k
 // atomics on one address serialised and cost ~300 us.)
 constexpr int kLongRun = 16, kFoldBatch = 8;
+#ifndef MAS_LONG_STEP
+#define MAS_LONG_STEP 256
+#endif
+constexpr int kLongStep = MAS_LONG_STEP, kLongK = kLongStep / 64, kLongStride = kLongStep + 1;  // long-run steps (below)
 
 // Fold targets: where the 3x3 of a key lives and its row stride.
 struct DenseEntry {  // block entry (row node, column node) of the dense buffer
@@ -787,7 +791,7 @@ template <class Tgt, bool kColMajor, class Key>
 __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __restrict__ keys,
                                                   const int* __restrict__ mats, const float* __restrict__ vals,
                                                   Tgt tgt) {
-    __shared__ float T[9 * 65];  // T[q * 65 + record]: component q (row-major); stride 65 keeps lanes 0..8 apart
+    __shared__ float T[9 * kLongStride];  // T[q * kLongStride + record]: component q (row-major)
     constexpr int S = Tgt::kStride;
     auto comp = [](int r, int c) { return kColMajor ? c * 3 + r : r * 3 + c; };
     const int lane = threadIdx.x;
@@ -826,27 +830,73 @@ __global__ __launch_bounds__(64) void k_fold_runs(int n, Key dead, const Key* __
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) e[r * S + c] = acc[r * 3 + c];
     }
-    // long runs: the whole wave, 64 records per step staged in LDS, lanes 0..8 fold
+    // long runs: the whole wave, kLongStep records per step (kLongK per lane,
+    // coalesced) staged in LDS, lanes 0..8 each folding one of the nine
+    // entries over them in order.  Software-pipelined: while a step is folded,
+    // the values of the next step and the keys / record ids of the one after
+    // it are in flight, so a step costs its fold, not the three dependent
+    // load latencies (keys -> ids -> values) it took when each 64-record step
+    // waited for its own loads (~4.5 us per step; the push and contact-entry
+    // folds' runs of ~1 000 records set a world-8 rank's Prepare chain).
     const int r = lane / 3, c = lane % 3;
     for (unsigned long long starts = __ballot(isLong); starts; starts &= starts - 1) {
         const int start = blockIdx.x * 64 + __ffsll((long long)starts) - 1;
         const Key lkey = keys[start];
         float* e = tgt.at(lkey, start);
         float acc = lane < 9 && !Tgt::kFromZero ? e[r * S + c] : 0.f;
-        for (int j0 = start;; j0 += 64) {
-            const int j = j0 + lane;
-            const bool in = j < n && keys[j] == lkey;
-            const int cnt = __popcll(__ballot(in));  // the run is contiguous: lanes 0..cnt-1
-            if (in) {
-                const float* src = vals + 9 * (size_t)mats[j];
+        auto loadKM = [&](int p0, bool (&in)[kLongK], int (&mt)[kLongK]) {
 #pragma unroll
-                for (int q = 0; q < 9; ++q) T[q * 65 + lane] = src[q];
+            for (int k = 0; k < kLongK; ++k) {
+                const int pos = p0 + 64 * k + lane;
+                in[k] = pos < n && keys[pos] == lkey;
+                mt[k] = pos < n ? mats[pos] : 0;
+            }
+        };
+        auto loadV = [&](const int (&mt)[kLongK], float (&v)[kLongK][9]) {
+#pragma unroll
+            for (int k = 0; k < kLongK; ++k) {
+                const float* src = vals + 9 * (size_t)mt[k];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) v[k][q] = src[q];
+            }
+        };
+        bool inA[kLongK], inB[kLongK];
+        int mA[kLongK], mB[kLongK];
+        float vA[kLongK][9];
+        loadKM(start, inA, mA);
+        loadV(mA, vA);
+        loadKM(start + kLongStep, inB, mB);
+        for (int p0 = start;; p0 += kLongStep) {
+            int cnt = 0;  // the run is contiguous: positions p0 .. p0 + cnt - 1
+#pragma unroll
+            for (int k = 0; k < kLongK; ++k) cnt += __popcll(__ballot(inA[k]));
+#pragma unroll
+            for (int k = 0; k < kLongK; ++k)
+                if (inA[k])
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) T[q * kLongStride + 64 * k + lane] = vA[k][q];
+            float vB[kLongK][9];
+            bool inC[kLongK];
+            int mC[kLongK];
+            if (cnt == kLongStep) {  // the next step's values, the one after's keys and ids
+                loadV(mB, vB);
+                loadKM(p0 + 2 * kLongStep, inC, mC);
             }
             __syncthreads();
-            if (lane < 9)
-                for (int k = 0; k < cnt; ++k) acc = __fadd_rn(acc, T[comp(r, c) * 65 + k]);
+            if (lane < 9) {
+                const float* col = T + comp(r, c) * kLongStride;
+                for (int k = 0; k < cnt; ++k) acc = __fadd_rn(acc, col[k]);
+            }
             __syncthreads();
-            if (cnt < 64) break;
+            if (cnt < kLongStep) break;
+#pragma unroll
+            for (int k = 0; k < kLongK; ++k) {
+                inA[k] = inB[k];
+                inB[k] = inC[k];
+                mB[k] = mC[k];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) vA[k][q] = vB[k][q];
+            }
         }
         if (lane < 9) e[r * S + c] = acc;
     }
@@ -987,14 +1037,20 @@ __global__ __launch_bounds__(256) void k_term_write_lanes(int l, int nV, const i
 #ifndef MAS_FOLD_CHUNK
 #define MAS_FOLD_CHUNK 256
 #endif
-constexpr int kFoldChunk = MAS_FOLD_CHUNK, kFoldStride = kFoldChunk + 4;
+// Levels with few nodes (a shard's level 3: 4 nodes at 1M) are one node's
+// dependent chain of ~10k terms; there a 256-term chunk's fold (~1 000
+// cycles) is shorter than the HBM latency the two-deep pipeline hides, so
+// they fold 1 024-term chunks (k_table_fold<kFoldChunkFew>, 37 KB of LDS).
+constexpr int kFoldChunkFew = 1024, kFoldFewNodes = 64;
 
+template <int kFoldChunk>
 __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, int beginPrev,
                                                    const int* __restrict__ vlist, const int* __restrict__ voff,
                                                    const int* __restrict__ termOff, const int* __restrict__ terms,
                                                    const int* __restrict__ cstPrev2, const int* __restrict__ gn,
                                                    const float* __restrict__ off9, const float* __restrict__ od,
                                                    float* __restrict__ tab, float* __restrict__ dense, int local0) {
+    constexpr int kFoldStride = kFoldChunk + 4;
     __shared__ __attribute__((aligned(16))) float st[9 * kFoldStride];
     const int local = local0 + blockIdx.x;
     const int lane = threadIdx.x;
@@ -1089,6 +1145,17 @@ __global__ __launch_bounds__(64) void k_table_fold(int l, int count, int begin, 
             *d = __fadd_rn(*d, acc);
         }
     }
+}
+
+static void table_fold(int cnt, int l, int count, int begin, int beginPrev, const int* vlist, const int* voff,
+                       const int* termOff, const int* terms, const int* cstPrev2, const int* gn, const float* off9,
+                       const float* od, float* tab, float* dense, int local0, hipStream_t s) {
+    if (cnt <= kFoldFewNodes)
+        k_table_fold<kFoldChunkFew><<<cnt, 64, 0, s>>>(l, count, begin, beginPrev, vlist, voff, termOff, terms,
+                                                       cstPrev2, gn, off9, od, tab, dense, local0);
+    else
+        k_table_fold<MAS_FOLD_CHUNK><<<cnt, 64, 0, s>>>(l, count, begin, beginPrev, vlist, voff, termOff, terms,
+                                                        cstPrev2, gn, off9, od, tab, dense, local0);
 }
 
 template <class T>
@@ -1499,6 +1566,10 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                                (rc = hip_check(h, hipEventCreateWithFlags(&h->evFoldFork, hipEventDisableTiming),
                                                "fold event")) ||
                                (rc = hip_check(h, hipEventCreateWithFlags(&h->evFoldJoin, hipEventDisableTiming),
+                                               "fold event")) ||
+                               (rc = hip_check(h, hipEventCreateWithFlags(&h->evDiag1, hipEventDisableTiming),
+                                               "fold event")) ||
+                               (rc = hip_check(h, hipEventCreateWithFlags(&h->evPreJoin, hipEventDisableTiming),
                                                "fold event"))))
             return rc;
         const RecKey rk0{h->levelSize[3], bit_width((unsigned)(tc - h->levelSize[3]))};
@@ -1567,16 +1638,28 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
                 DenseEntry{dense, rk});
         if (bank1 > bank0)
             k_diag1<<<cdiv(bank1 - bank0, 256), 256, 0, s>>>(nV, gn, P<float>(h->od), dense, bank0, bank1);
+        // The coarse split's level-1 blocks that only this rank has rows in are
+        // complete now (contacts, the records' fold, k_diag1: the table folds
+        // write level >= 2 diagonals only), so their factor runs on the side
+        // stream beside the table folds, whose level-3 fold is one node's
+        // dependent chain (~0.1 ms at 1M) however the rows are split
+        if (sideFold && h->splitPlanned && h->splitPre.size() == 2 && L > 2) {
+            if ((rc = hip_check(h, hipEventRecord(h->evDiag1, s), "diag1 done")) ||
+                (rc = hip_check(h, hipStreamWaitEvent(h->foldStream, h->evDiag1, 0), "pre-factor wait")) ||
+                (rc = factor_blocks(h, h->splitPre[0], h->splitPre[1], h->foldStream)) ||
+                (rc = hip_check(h, hipEventRecord(h->evPreJoin, h->foldStream), "pre-factor join")))
+                return rc;
+            h->preFactored = true;
+        }
         for (int l = 2; l < L; ++l) {
             const int count = h->levelSize[2 * l], begin = h->levelSize[2 * l + 1];
             const int beginPrev = h->levelSize[2 * (l - 1) + 1];
             int local0 = 0, cnt = 0;
             nodeRange(l, local0, cnt);
             if (cnt > 0)
-                k_table_fold<<<cnt, 64, 0, s>>>(l, count, begin, beginPrev, P<int>(h->vlistL[l]),
-                                                P<int>(h->voffL[l]), P<int>(h->termOffL[l]), P<int>(h->termsL[l]),
-                                                P<int>(h->cst) + (size_t)(l - 2) * nV, gn, d_off9, P<float>(h->od),
-                                                P<float>(h->tab), dense, local0);
+                table_fold(cnt, l, count, begin, beginPrev, P<int>(h->vlistL[l]), P<int>(h->voffL[l]),
+                           P<int>(h->termOffL[l]), P<int>(h->termsL[l]), P<int>(h->cst) + (size_t)(l - 2) * nV, gn,
+                           d_off9, P<float>(h->od), P<float>(h->tab), dense, local0, s);
         }
         h->recHierId = h->hierId;
         h->recShardKey = shardKey;
@@ -1671,8 +1754,8 @@ int run_assemble(mas_context* h, const float* d_diag9, const float* d_off9, cons
         int local0 = 0, cnt = 0;
         nodeRange(l, local0, cnt);
         if (cnt > 0)
-            k_table_fold<<<cnt, 64, 0, s>>>(l, count, begin, beginPrev, vlist, voff, termOff, terms, cstPrev2, gn,
-                                            d_off9, P<float>(h->od), P<float>(h->tab), dense, local0);
+            table_fold(cnt, l, count, begin, beginPrev, vlist, voff, termOff, terms, cstPrev2, gn, d_off9,
+                       P<float>(h->od), P<float>(h->tab), dense, local0, s);
     }
     h->nRecCached = nRec;
     h->recHierId = h->hierId;

@@ -779,6 +779,7 @@ int run_factor(mas_context* h, hipStream_t s) {
     int rc;
     if (!fused && (rc = factor_blocks(h, h->fineBlk0, h->fineBlk1, s))) return rc;
     if (h->splitPlanned) {
+        if (h->preFactored) return MAS_OK;  // on foldStream already (run_assemble)
         for (size_t i = 0; i + 1 < h->splitPre.size(); i += 2)
             if ((rc = factor_blocks(h, h->splitPre[i], h->splitPre[i + 1], s))) return rc;
         return MAS_OK;

@@ -63,7 +63,10 @@ constexpr int kPcgThreads = MAS_PCG_THREADS;
 #ifndef MAS_SPMV_NT
 #define MAS_SPMV_NT 1
 #endif
-constexpr int kPcgBlocks = 1024;  // fixed grid: partial sums in a fixed order
+#ifndef MAS_PCG_BLOCKS
+#define MAS_PCG_BLOCKS 1024
+#endif
+constexpr int kPcgBlocks = MAS_PCG_BLOCKS;  // fixed grid: partial sums in a fixed order
 
 struct PcgState {
     double rz[2];  // r.z of the current / next iteration (slot it & 1)
@@ -474,6 +477,17 @@ __device__ __forceinline__ float4 p_next(float beta, float4 pv, float4 zv) {
 }
 
 // Ap = A p; partials p.Ap
+// Occupancy: the fused form needs 70 VGPRs, i.e. 7 waves per SIMD, so a CU
+// holds three of the fixed grid's 512-thread workgroups and the last quarter
+// of the 1 024 runs as a second, quarter-full round.  Capped at 64 VGPRs (8
+// waves per SIMD, 12 bytes per lane spilled: MAS_SPMV_WAVES=8) all 1 024 are
+// resident at once, but the spills cost more: 1M + contacts 0.2280-0.2304 ->
+// 0.2364-0.2365 ms per MAS iteration, unpreconditioned 0.1130-0.1155 ->
+// 0.1217 (profiles/round6/ab/pcg_spmv_waves/).  0 (the default): no cap.
+#ifndef MAS_SPMV_WAVES
+#define MAS_SPMV_WAVES 0
+#endif
+constexpr int kSpmvWaves = MAS_SPMV_WAVES > 0 ? MAS_SPMV_WAVES : 1;
 #ifndef MAS_SPMV_PIPE
 #define MAS_SPMV_PIPE 1
 #endif
@@ -500,7 +514,7 @@ __device__ __forceinline__ void ell_load(int g0, int lane, const float* __restri
 // intact for the other rows' gathers).  One launch and one pass over z and p
 // less per iteration; the iterates are bitwise those of the unfused form.
 template <int G, bool FUSE>
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_spmv(int nV, const int* __restrict__ starts,
+__global__ __launch_bounds__(kPcgThreads) __attribute__((amdgpu_waves_per_eu(kSpmvWaves))) void k_pcg_spmv(int nV, const int* __restrict__ starts,
                                                           const int* __restrict__ idx, const float* __restrict__ diag,
                                                           const float* __restrict__ off,
                                                           const float* __restrict__ ellOff,

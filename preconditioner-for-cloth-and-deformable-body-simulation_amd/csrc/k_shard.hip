@@ -429,15 +429,21 @@ int mas_apply_shard_complete(mas_handle h, int rank, int world, const float* d_g
     return hip_check(h, hipGetLastError(), "shard complete");
 }
 
-// The whole per-rank apply with the collective inside (include/mas_capi.h):
-// restrict on `stream`, then on the handle's communication stream (which
-// waits for the restrict) the allgather hook and right behind it the coarse
-// levels (k_shard_coarse12 needs only the gathered R1), while `stream` solves
-// the own level-0 blocks; `stream` waits for the coarse levels only before the
-// prolongation.  (Round 5 ran the coarse launch on `stream` after the level-0
-// solves it does not depend on: 15.2 us of replicated coarse work after them
-// per world-8 rank at 1M + contacts.)  One rank has nothing to hide: the
-// serial form.
+// The whole per-rank apply with the collective inside (include/mas_capi.h).
+// Default (shardMode 0): everything on `stream` -- restrict, the allgather
+// hook enqueued on `stream` itself, the coarse levels, the own level-0 blocks
+// with the prolongation fused (mas_apply_shard_finish).  No cross-stream
+// dependency: on MI355X a hipStreamWaitEvent hop between two queues measured
+// ~14 us each (world-8 rank at 1M + contacts with the loopback collective:
+// inline 31 us per apply; the collective on a communication stream joined
+// back by events 60 us; profiles/round6/shard/), and a level-0 kernel queued
+// beside the collective fills every CU, so the collective's kernel starts
+// only as it drains (the same as the round-1 probe of a kernel queued behind
+// an 8k-workgroup one: 50-70 us late).  shardMode 1 / 2 (env
+// MAS_SHARD_MODE, A/B): the collective on the handle's communication stream
+// while `stream` solves the own level-0 blocks, the coarse levels on the
+// communication stream behind it (1) or on `stream` after the solves (2, the
+// round-5 form), `stream` joining before the prolongation.
 int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn allgather, void* user, float* d_z4,
                            const float* d_r4, void* stream) {
     if (!h) return MAS_ERR_ARG;
@@ -486,14 +492,19 @@ int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn a
             return rc;
         return mas_apply_shard_finish(h, rank, world, gathered, d_r4, d_z4, s);
     }
+    if (h->shardMode == 0) {  // inline: the collective on `stream`, then the rest behind it
+        if (int e = allgather(seg, gathered, segBytes, s, user))
+            return fail(h, MAS_ERR_COMM, "allgather hook returned " + std::to_string(e));
+        return mas_apply_shard_finish(h, rank, world, gathered, d_r4, d_z4, s);
+    }
     if ((rc = hip_check(h, hipEventRecord(h->evRestrict, s), "record")) ||
         (rc = hip_check(h, hipStreamWaitEvent(h->commStream, h->evRestrict, 0), "comm wait")))
         return rc;
     if (int e = allgather(seg, gathered, segBytes, h->commStream, user))
         return fail(h, MAS_ERR_COMM, "allgather hook returned " + std::to_string(e));
-    // the coarse levels on the communication stream, behind the gather
-    // (env MAS_SHARD_COARSE_SIDE=0: on `stream` after the level-0 solves, A/B)
-    const bool side = h->shardCoarseSide != 0;
+    // the coarse levels on the communication stream behind the gather (1) or
+    // on `stream` after the level-0 solves (2)
+    const bool side = h->shardMode == 1;
     if (side && h->L > 1 && (rc = shard_coarse(h, sh, world, gathered, h->commStream))) return rc;
     if ((rc = hip_check(h, hipEventRecord(h->evGathered, h->commStream), "record")) ||
         (rc = mas_apply_shard_fine(h, rank, world, d_r4, d_z4, s)) ||

@@ -210,7 +210,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_FOLD_SIDE")) h->foldSide = std::atoi(v);
     if (const char* v = std::getenv("MAS_HIER_CACHE")) h->hierCache = std::atoi(v);
     if (const char* v = std::getenv("MAS_HOST_REGISTER")) h->hostRegister = std::atoi(v);
-    if (const char* v = std::getenv("MAS_SHARD_COARSE_SIDE")) h->shardCoarseSide = std::atoi(v);
+    if (const char* v = std::getenv("MAS_SHARD_MODE")) h->shardMode = std::atoi(v);
     // MAS_PREP_SERIAL=1 (A/B) queues the early path on the caller's stream: from
     // one host thread, so the launch order on that stream is fixed
     if (const char* v = std::getenv("MAS_PREP_SERIAL"))
@@ -249,11 +249,14 @@ int mas_destroy(mas_handle h) {
     }
     if (h->evFoldFork) hipEventDestroy(h->evFoldFork);
     if (h->evFoldJoin) hipEventDestroy(h->evFoldJoin);
+    if (h->evDiag1) hipEventDestroy(h->evDiag1);
+    if (h->evPreJoin) hipEventDestroy(h->evPreJoin);
     for (auto& e : h->evFine)
         if (e) hipEventDestroy(e);
     release_comm(h);  // drained above; the communicator goes before the buffers it wrote
     for (auto& q : h->pins)
         if (q.registered) hipHostUnregister(const_cast<void*>(q.p));
+    (void)hipGetLastError();
     h->for_each_buffer([](Buffer& b) { release(b); });
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
@@ -296,22 +299,34 @@ int mas_allocate(mas_handle h, int nV, int nE, int nF, const float* pos4, const 
 
 // Page-lock the caller's host array of slot `slot` (mas_context::pins) so the
 // copies of the host-pointer entry points run at the pinned rate instead of
-// through the runtime's pageable staging.  Memory that is pinned already
-// (hipHostMalloc, a torch pinned tensor) or cannot be registered is used as
-// it is: registration only changes the copy rate, never the result.
+// through the runtime's pageable staging.  An array is registered the second
+// time it comes back in the same slot (same pointer and size): a caller that
+// passes a fresh temporary every call (a Python binding's output array) never
+// pays a registration per call.  Memory that is pinned already (hipHostMalloc,
+// a torch pinned tensor) or cannot be registered is used as it is:
+// registration only changes the copy rate, never the result, and no error of
+// these calls is left behind for the caller's next HIP check.
 static void pin_host(mas_context* h, int slot, const void* p, size_t bytes) {
     if (!h->hostRegister || !p || !bytes) return;
     auto& q = h->pins[slot];
-    if (q.p == p && q.bytes == bytes) return;
-    if (q.registered) hipHostUnregister(const_cast<void*>(q.p));
-    q.p = p;
-    q.bytes = bytes;
-    q.registered = false;
+    if (q.p != p || q.bytes != bytes) {
+        if (q.registered) {
+            hipHostUnregister(const_cast<void*>(q.p));
+            (void)hipGetLastError();  // the caller may have freed it already
+        }
+        q.p = p;
+        q.bytes = bytes;
+        q.registered = false;
+        q.seen = 1;
+        return;
+    }
+    if (q.registered || q.seen++ != 1) return;  // registered, or found unregistrable
     for (const auto& o : h->pins)  // one registration per array (z and r may be one buffer)
         if (&o != &q && o.registered && o.p == p) return;
     hipPointerAttribute_t attr{};
-    if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost) return;
+    const bool pinned = hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost;
     (void)hipGetLastError();
+    if (pinned) return;
     q.registered = hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) == hipSuccess;
     (void)hipGetLastError();  // a refused registration leaves the copy pageable, not an error
 }

@@ -299,6 +299,10 @@ struct mas_context {
     int foldSide = -1;
     hipStream_t foldStream = nullptr;
     hipEvent_t evFoldFork = nullptr, evFoldJoin = nullptr;
+    // the coarse split's pre level-1 factor, on foldStream beside the table
+    // folds (run_assemble); run_prepare joins it last (evPreJoin)
+    hipEvent_t evDiag1 = nullptr, evPreJoin = nullptr;
+    bool preFactored = false;
     mas::Buffer add0, c0Cnt, c0Off, c0Keys, c0KeysS, c0Ids, c0IdsS, c0Val, a0Keys, a0KeysS, a0Ids, a0IdsS, a0Val;
     mas::Buffer additional, od, recCnt, recOff, rec, recKeys, recKeysSorted, recIds, recIdsSorted;
     mas::Buffer vkeys, tab, termCnt;
@@ -377,7 +381,10 @@ struct mas_context {
     // the communication stream and its fork/join events
     mas::Buffer shardSeg, shardGathered;
     hipStream_t commStream = nullptr;
-    int shardCoarseSide = 1;  // the sharded apply's coarse levels on commStream (env MAS_SHARD_COARSE_SIDE=0: on the apply stream)
+    // mas_shard_apply_device (k_shard.hip): 0 = the collective and every kernel on the apply stream (default);
+    // 1 / 2 = the collective on commStream beside the level-0 solves, the coarse levels on commStream (1) or
+    // on the apply stream (2) (env MAS_SHARD_MODE, A/B)
+    int shardMode = 0;
     hipEvent_t evRestrict = nullptr, evGathered = nullptr;
     // end of the previous mas_shard_apply_device call and the stream it ran
     // on: a call on another stream waits for it (the segments are the handle's)
@@ -400,6 +407,7 @@ struct mas_context {
         const void* p = nullptr;
         size_t bytes = 0;
         bool registered = false;
+        int seen = 0;  // calls in a row with this (pointer, size); registered at the second
     } pins[7];
     int hostRegister = 1;
     // hipcub scratch

@@ -21,7 +21,11 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
     h->err.clear();  // after a successful Prepare: empty, or the non-SPD warning
     // a previous Prepare that failed between the side fold's fork and join
     // (run_assemble) may have left it running: this Prepare's memsets wait
-    if (h->foldStream) hipStreamWaitEvent(s, h->evFoldJoin, 0);
+    if (h->foldStream) {
+        hipStreamWaitEvent(s, h->evFoldJoin, 0);
+        if (h->preFactored) hipStreamWaitEvent(s, h->evPreJoin, 0);
+    }
+    h->preFactored = false;
     hipEventRecord(h->ev[2], s);
     // pivot checks of this Prepare's factors: [0] count, [1] lowest block (k_factor.hip check_pivots)
     int* status = P<int>(h->devStatus);
@@ -133,8 +137,9 @@ int run_prepare(mas_context* h, const float* d_diag9, const float* d_off9, const
         h->l1First.clear();  // per-bank level-1 starts: computed on first use (sharding, blob save)
         h->shardWorld = 0;
     }
-    // the fused level-0 kernel (prepStream) joins last: nothing above needs
-    // the level-0 inverses
+    // the side stream's level-1 factor (coarse split) and the fused level-0
+    // kernel (prepStream) join last: nothing above needs their inverses
+    if (h->preFactored && (rc = hip_check(h, hipStreamWaitEvent(s, h->evPreJoin, 0), "join pre factor"))) return rc;
     if (h->factorVariant >= 4 && (rc = hip_check(h, hipStreamWaitEvent(s, h->evPrepJoin, 0), "join fused factor")))
         return rc;
     hipEventRecord(h->ev[3], s);

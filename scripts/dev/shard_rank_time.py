@@ -2,7 +2,7 @@
 rank g of a world of W runs restrict -> (allgather replaced by a device copy
 of its own segment; the communication is NOT in these numbers) -> finish;
 mode one_call: mas_shard_apply_device with the loopback stand-in
-(mas_allgather_loopback), the coarse levels on the communication stream.
+(mas_allgather_loopback), in the stream form MAS_SHARD_MODE selects.
 Prints ms per apply for every (W, g) so the critical path of an N-GPU apply
 can be read as max_g(compute) + allgather.  Dev tool; GPU only."""
 import json
@@ -35,7 +35,7 @@ for W, mode in [(w, m) for w in worlds for m in modes]:
         dst = gathered[g * plan["seg_max"]:(g + 1) * plan["seg_max"]]
 
         def step():
-            if mode == "one_call":  # mas_shard_apply_device: coarse levels on the comm stream (round 6)
+            if mode == "one_call":  # mas_shard_apply_device (MAS_SHARD_MODE)
                 P.shard_apply_loopback(g, W, z, r, s.cuda_stream)
                 return
             P.shard_restrict(g, W, r, seg, s.cuda_stream)

@@ -5,6 +5,7 @@
 // iteration count are written back for comparison with the oracle.
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <string>
 #include <vector>
@@ -45,6 +46,19 @@ int main(int argc, char** argv) {
     std::vector<SeVec3fSimd> z(nV);
     P.Preconditioning(z.data(), r0.data(), 3 * nV);
     std::ofstream(d + "/z.bin", std::ios::binary).write(reinterpret_cast<const char*>(z.data()), z.size() * 16);
+    // the host-pointer path again: the caller's arrays are page-locked on
+    // their second use and reused from the library's cache (mas_capi.hip pin_host),
+    // a second Prepare through the same arrays, another output array
+    {
+        std::vector<SeVec3fSimd> z2(nV), z3(nV);
+        P.Preconditioning(z2.data(), r0.data(), 3 * nV);
+        P.PreparePreconditioner(diag.data(), off.data(), starts.data(), nullptr, nullptr, nullptr, efC.data(),
+                                eeC.data(), vfC.data());
+        P.Preconditioning(z3.data(), r0.data(), 3 * nV);
+        const bool same = std::memcmp(z.data(), z2.data(), z.size() * 16) == 0 &&
+                          std::memcmp(z.data(), z3.data(), z.size() * 16) == 0;
+        std::printf("host_repeat_bitwise %d\n", same ? 1 : 0);
+    }
 
     // PCG (float64 vectors, fp32 preconditioner) on H x = r0
     auto matvec = [&](const std::vector<double>& x, std::vector<double>& y) {

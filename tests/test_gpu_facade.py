@@ -34,5 +34,8 @@ def test_cpp_facade_pcg(tmp_path):
     z_ref = o.apply(r)
     err = np.linalg.norm(z[:, :3] - z_ref[:, :3]) / np.linalg.norm(z_ref[:, :3])
     assert err <= 1e-5, err
+    # Preconditioning / PreparePreconditioner repeated through the same host
+    # arrays (page-locked and cached by the library): bitwise the first z
+    assert "host_repeat_bitwise 1" in out, out
     iters = int(out.split("pcg_iterations")[1])
     assert 20 < iters < 200, out

@@ -184,24 +184,28 @@ def test_sharded_apply_helper_overlap_world1():
         assert np.array_equal(z.cpu().numpy(), P.Preconditioning(None, r.cpu().numpy())), overlap
 
 
-@pytest.mark.parametrize("kind,W,L,worlds,nc,refr", [("cloth", 100, 3, (1, 2, 3), 0, False),
-                                                     ("tet", 16, 3, (2, 8), 0, False),
-                                                     ("cloth", 1024, 4, (8,), 100_000, False),
-                                                     ("cloth", 1024, 4, (8,), 100_000, True),
-                                                     ("tet", 160, 4, (8,), 0, False)])
-def test_one_call_shard_apply_bitwise(kind, W, L, worlds, nc, refr):
-    """mas_shard_apply_device (the collective inside the library; the coarse
-    levels on its communication stream right behind the gather, beside the
-    level-0 solves on the apply stream): with an in-process allgather hook --
-    it writes every rank's segment into `recv` through the step-wise restrict,
-    so all ranks' calls run in one process -- the union of the ranks' own z
-    entries equals the unsharded apply bitwise, with the grouped level 3 and
-    the reference's (refr).  World 1 through the loopback stand-in takes the
-    same two-stream path."""
+@pytest.mark.parametrize("kind,W,L,worlds,nc,refr,mode", [("cloth", 100, 3, (1, 2, 3), 0, False, 0),
+                                                          ("tet", 16, 3, (2, 8), 0, False, 0),
+                                                          ("cloth", 100, 3, (2, 3), 0, False, 1),
+                                                          ("cloth", 1024, 4, (8,), 100_000, False, 0),
+                                                          ("cloth", 1024, 4, (8,), 100_000, False, 1),
+                                                          ("cloth", 1024, 4, (8,), 100_000, False, 2),
+                                                          ("cloth", 1024, 4, (8,), 100_000, True, 0),
+                                                          ("tet", 160, 4, (8,), 0, False, 0)])
+def test_one_call_shard_apply_bitwise(kind, W, L, worlds, nc, refr, mode, monkeypatch):
+    """mas_shard_apply_device (the collective inside the library): with an
+    in-process allgather hook -- it writes every rank's segment into `recv`
+    through the step-wise restrict, so all ranks' calls run in one process --
+    the union of the ranks' own z entries equals the unsharded apply bitwise,
+    with the grouped level 3 and the reference's (refr), in every stream form
+    (MAS_SHARD_MODE: 0 everything on the apply stream, the default; 1 / 2 the
+    collective on the communication stream with the coarse levels behind it
+    or after the level-0 solves).  World 1 through the loopback stand-in."""
     import torch
     import mas_amd
     from mas_amd import meshgen
     from mas_amd.distributed import device_view
+    monkeypatch.setenv("MAS_SHARD_MODE", str(mode))
     mesh = cloth(W) if kind == "cloth" else tet(W)
     contacts = meshgen.vf_contacts(mesh, nc, seed=3) if nc else None
     P = mas_amd.from_mesh(mesh, max_levels=L, contacts=contacts, reference_restriction=refr)
