@@ -154,6 +154,13 @@ constexpr int kSpmvRows = 1;  // row groups per wave and pass
 // load no longer waits for starts.  Entries j >= G (rows longer than G) stay
 // in the CSR arrays.  Same entries on the same lanes in the same order:
 // bitwise equal to the CSR form.
+// MAS_ELL2 (A/B): the neighbour id and the nine components as five float2
+// rows per group (640 floats, the same bytes as 576 + 64): five 8-byte loads
+// per lane and pass instead of ten 4-byte ones
+#ifndef MAS_ELL2
+#define MAS_ELL2 0
+#endif
+constexpr bool kEll2 = MAS_ELL2 != 0;
 template <int G>
 __global__ __launch_bounds__(256) void k_pcg_ell(int nV, int nGroups, const int* __restrict__ starts,
                                                  const int* __restrict__ idx, const float* __restrict__ off,
@@ -167,7 +174,18 @@ __global__ __launch_bounds__(256) void k_pcg_ell(int nV, int nGroups, const int*
         const int e0 = starts[v] + j;
         if (e0 < starts[v + 1]) e = e0;
     }
-    ellIdx[t] = e >= 0 ? idx[e] : -1;
+    const int nb = e >= 0 ? idx[e] : -1;
+    if (kEll2) {  // (nb, m0), (m1, m2), ..., (m7, m8) as five float2 rows of 64 slots
+        float2* dst = reinterpret_cast<float2*>(ellOff + (size_t)gi * 640) + slot;
+        float m[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) m[q] = e >= 0 ? off[9 * (size_t)e + q] : 0.f;
+        dst[0] = make_float2(__int_as_float(nb), m[0]);
+#pragma unroll
+        for (int k = 1; k < 5; ++k) dst[k * 64] = make_float2(m[2 * k - 1], m[2 * k]);
+        return;
+    }
+    ellIdx[t] = nb;
     float* dst = ellOff + (size_t)gi * 576 + slot;
 #pragma unroll
     for (int q = 0; q < 9; ++q) dst[q * 64] = e >= 0 ? off[9 * (size_t)e + q] : 0.f;
@@ -190,7 +208,18 @@ __device__ __forceinline__ void spmv_rows_ell(int base, int nV, int lane, const 
         v[r] = base + r * (64 / G) + lane / G;
         // the matrix streams once per SpMV (302 MB at 1M, beyond the Infinity
         // Cache): nontemporal, so it does not evict the gathered vector
-        if (MAS_SPMV_NT) {
+        if (kEll2) {
+            const float2* src = reinterpret_cast<const float2*>(ellOff + (size_t)(g0 + r) * 640) + lane;
+            const float2 w0 = src[0];
+            nb[r] = __float_as_int(w0.x);
+            m[r][0] = w0.y;
+#pragma unroll
+            for (int k = 1; k < 5; ++k) {
+                const float2 w = src[k * 64];
+                m[r][2 * k - 1] = w.x;
+                m[r][2 * k] = w.y;
+            }
+        } else if (MAS_SPMV_NT) {
             nb[r] = __builtin_nontemporal_load(ellIdx + (size_t)(g0 + r) * 64 + lane);
 #pragma unroll
             for (int q = 0; q < 9; ++q)
@@ -500,6 +529,21 @@ struct EllSlot {
 template <int G>
 __device__ __forceinline__ void ell_load(int g0, int lane, const float* __restrict__ ellOff,
                                          const int* __restrict__ ellIdx, EllSlot& e) {
+    if (kEll2) {
+        typedef float v2 __attribute__((ext_vector_type(2)));
+        const v2* src = reinterpret_cast<const v2*>(ellOff + (size_t)g0 * 640) + lane;
+        const v2 w0 = __builtin_nontemporal_load(src);
+        e.nb = __float_as_int(w0.x);
+        e.m[0] = w0.y;
+        __builtin_amdgcn_sched_barrier(0);  // nb first: the gathers wait for it alone
+#pragma unroll
+        for (int k = 1; k < 5; ++k) {
+            const v2 w = __builtin_nontemporal_load(src + k * 64);
+            e.m[2 * k - 1] = w.x;
+            e.m[2 * k] = w.y;
+        }
+        return;
+    }
     e.nb = __builtin_nontemporal_load(ellIdx + (size_t)g0 * 64 + lane);
     __builtin_amdgcn_sched_barrier(0);  // nb first: the gathers wait for it alone
 #pragma unroll
@@ -700,7 +744,7 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     // the last pass may read up to kSpmvRows - 1 groups past the rows: they
     // are allocated and filled as empty slots (idx -1)
     const int nGroups = cdiv(nV, 64 / G) + kSpmvRows;
-    if ((rc = ensure(h, h->pcgEllOff, (size_t)nGroups * 576 * 4)) ||
+    if ((rc = ensure(h, h->pcgEllOff, (size_t)nGroups * 640 * 4)) ||
         (rc = ensure(h, h->pcgEllIdx, (size_t)nGroups * 64 * 4)))
         return rc;
     float* ellOff = P<float>(h->pcgEllOff);

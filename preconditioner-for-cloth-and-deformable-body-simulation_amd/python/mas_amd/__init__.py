@@ -364,6 +364,23 @@ class SeSchwarzPreconditioner:
         self._rows_pending = False
         self._warn_prepare("prepare_shard_complete")
 
+    def set_prepare_allgather(self, allgather):
+        """allgather(send_ptr, recv_ptr, nbytes, stream_ptr) -> None, enqueued on
+        that stream: a sharded Prepare then exchanges its coarse rows inside
+        Prepare (mas_set_prepare_allgather); None removes it."""
+        if allgather is None:
+            fn = ALLGATHER_FN()
+        else:
+            def hook(send, recv, nbytes, strm, _user):
+                try:
+                    allgather(send, recv, nbytes, strm)
+                    return 0
+                except Exception:  # reported as MAS_ERR_COMM by the Prepare
+                    return 1
+            fn = ALLGATHER_FN(hook)
+        self._prep_hook = fn  # the callback must outlive every Prepare that calls it
+        self._check(self._L.mas_set_prepare_allgather(self.h, fn, None), "set_prepare_allgather")
+
     @property
     def rows_pending(self) -> bool:
         return self._rows_pending

@@ -291,9 +291,12 @@ def test_rccl_transport_world1():
 
 
 def test_two_processes_gloo_drive_library():
-    """Two ranks as two processes on this GPU, gloo allgather hook: each rank
-    runs the library's one-call sharded apply (its own handle, kernels on the
-    GPU) and checks its own z entries bitwise against its unsharded apply."""
+    """Two ranks as two processes on this GPU, gloo: each rank prepares its
+    own shard (own level-0 blocks, own coarse rows), exchanges the coarse rows
+    with the other process (mas_prepare_shard_rows / _complete through
+    torch.distributed), runs the library's one-call sharded apply with a gloo
+    allgather hook, and checks its own z entries bitwise against an unsharded
+    handle's apply."""
     import os
     import subprocess
     import sys
@@ -313,3 +316,52 @@ def test_two_processes_gloo_drive_library():
     for p, out in zip(procs, outs):
         assert p.returncode == 0, out[-3000:]
         assert "SHARD_OK" in out, out[-3000:]
+
+
+def test_prepare_exchange_inside_prepare():
+    """The coarse-row exchange run inside mas_prepare through a registered
+    allgather hook (mas_set_prepare_allgather): rank 0 of a world of 2 whose
+    hook delivers both ranks' segments (taken from two-phase rank handles)
+    ends its Prepare with nothing pending, and its coarse inverses equal the
+    unsharded handle's bitwise; a failing hook fails the Prepare with
+    MAS_ERR_COMM."""
+    import torch
+    import mas_amd
+    from mas_amd import meshgen
+    from mas_amd.distributed import device_view
+    mesh = cloth(128)
+    contacts = meshgen.vf_contacts(mesh, 500, seed=3)
+    Pf = mas_amd.from_mesh(mesh, max_levels=4, contacts=contacts)
+    two = [mas_amd.from_mesh(mesh, max_levels=4, contacts=contacts, shard=(g, 2)) for g in range(2)]
+    segs = [Pg.prepare_shard_rows() for Pg in two]
+    nbytes = segs[0][1]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    gathered = torch.cat([device_view(ptr, nbytes // 4, dev).clone() for ptr, _ in segs])
+    calls = []
+
+    def hook(send, recv, nb, strm):
+        calls.append(nb)
+        with torch.cuda.stream(torch.cuda.ExternalStream(strm, device=dev)):
+            device_view(recv, 2 * nb // 4, dev).copy_(gathered)
+
+    P0 = mas_amd.SeSchwarzPreconditioner(max_levels=4)
+    P0.set_prepare_shard(0, 2)
+    P0.set_prepare_allgather(hook)
+    P0.m_positions, P0.m_neighbours, P0.m_edges, P0.m_faces = mesh.pos, (mesh.starts, mesh.idx), mesh.edges, mesh.faces
+    P0.AllocatePrecoditioner(mesh.nV, mesh.edges.shape[0], mesh.faces.shape[0])
+    vf, vfC = contacts
+    P0.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, vf, None, None, vfC)
+    assert calls == [nbytes] and not P0.rows_pending and P0.stats()["coarse_split"] in (1, 2)
+    info = Pf.info()
+    ls, nblk = info["level_size"], info["num_blocks"]
+    plan = P0.shard_setup(0, 2)
+    b1 = int(ls[1][1]) // 32
+    for a, b in ((b1 + plan["l1_begin"] // 32, b1 + (plan["l1_end"] + 31) // 32), (int(ls[2][1]) // 32, nblk)):
+        assert np.array_equal(P0.packed_inverses(a, b - a).view(np.uint32), Pf.packed_inverses(a, b - a).view(np.uint32))
+
+    def broken(*a):
+        raise RuntimeError("link down")
+
+    P0.set_prepare_allgather(broken)
+    with pytest.raises(mas_amd.MasError, match="COMM"):
+        P0.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, vf, None, None, vfC)
