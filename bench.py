@@ -191,37 +191,51 @@ def cpu_baseline(mesh, cfg, contacts, r_np, steps):
     return out, z
 
 
+def page_aligned(a):
+    """A copy of `a` starting on a page boundary, its buffer covering the last
+    page whole (what mas_config.host_register asks of the caller)."""
+    import numpy as np
+    n = a.nbytes
+    buf = np.empty(n + (-n) % 4096 + 4096, np.uint8)
+    off = (-buf.ctypes.data) % 4096
+    v = buf[off:off + n].view(a.dtype).reshape(a.shape)
+    v[...] = a
+    return v
+
+
 def host_path(P, mesh, contacts, r_np, make_handle, reps=5, applies=20):
     """The drop-in host-pointer path (SeSchwarzPreconditioner.h:59-63): a PCG
     loop that already calls the reference passes host arrays, so Prepare
     copies the CSR Hessian H2D and every apply copies r in and z out.  Wall
     time of the synchronous calls, median of `reps` Prepares / `applies`
-    applies after the first (the second call with the same arrays page-locks them,
-    mas_capi.hip pin_host); the same with MAS_HOST_REGISTER=0 (the runtime's
-    pageable staging) on a second handle for comparison."""
+    applies after the first, on the default handle (the runtime's pageable
+    staging) and on a second handle with mas_config.host_register = 1 and
+    page-aligned arrays (registered at their second call, mas_capi.hip
+    pin_host)."""
     import numpy as np
 
-    def prep(h):
-        if contacts is None:
-            h.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
-        else:
-            h.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, contacts[0], None, None, contacts[1])
+    def measure(h, diag, off, starts, r, cts):
+        z_np = page_aligned(np.zeros_like(r))
 
-    def measure(h):
-        z_np = np.empty_like(r_np)
+        def prep():
+            if cts is None:
+                h.PreparePreconditioner(diag, off, starts)
+            else:
+                h.PreparePreconditioner(diag, off, starts, None, None, cts[0], None, None, cts[1])
+
         t = time.perf_counter()
-        prep(h)
+        prep()
         first = time.perf_counter() - t
         tp, ta = [], []
         for _ in range(reps):
             t = time.perf_counter()
-            prep(h)
+            prep()
             tp.append(time.perf_counter() - t)
         dev_ms = h.stats()["prepare_ms"]
-        h.Preconditioning(z_np, r_np)
+        h.Preconditioning(z_np, r)
         for _ in range(applies):
             t = time.perf_counter()
-            h.Preconditioning(z_np, r_np)
+            h.Preconditioning(z_np, r)
             ta.append(time.perf_counter() - t)
         return {"prepare_ms_incl_h2d": round(statistics.median(tp) * 1e3, 3),
                 "prepare_first_call_ms_incl_h2d": round(first * 1e3, 3),
@@ -229,19 +243,17 @@ def host_path(P, mesh, contacts, r_np, make_handle, reps=5, applies=20):
                 "apply_ms_incl_pcie": round(statistics.median(ta) * 1e3, 4)}, z_np
 
     nV, nnz = mesh.nV, int(mesh.starts[-1])
-    pinned, z1 = measure(P)
-    os.environ["MAS_HOST_REGISTER"] = "0"
-    try:
-        P2 = make_handle()
-        pageable, z2 = measure(P2)
-        del P2
-    finally:
-        del os.environ["MAS_HOST_REGISTER"]
-    return {**pinned, "pageable": pageable,
-            "z_bitwise_pinned_vs_pageable": bool(np.array_equal(z1.view(np.uint32), z2.view(np.uint32))),
+    pageable, z1 = measure(P, mesh.diag, mesh.off, mesh.starts, r_np, contacts)
+    P2 = make_handle(host_register=True)
+    registered, z2 = measure(P2, page_aligned(mesh.diag), page_aligned(mesh.off), page_aligned(mesh.starts),
+                             page_aligned(r_np), contacts)
+    del P2
+    return {**pageable, "registered": registered,
+            "z_bitwise_registered_vs_pageable": bool(np.array_equal(z1.view(np.uint32), z2.view(np.uint32))),
             "h2d_bytes_prepare": nV * 36 + nnz * 36 + (nV + 1) * 4, "pcie_bytes_apply": 2 * 16 * nV,
-            "note": "host arrays through mas_prepare / mas_apply (synchronous), wall clock; the caller's arrays "
-                    "are page-locked when passed a second time and cached by (pointer, size); value and roofline use "
+            "note": "host arrays through mas_prepare / mas_apply (synchronous), wall clock; top level: the default "
+                    "handle (pageable staging by the runtime); registered: mas_config.host_register = 1 with "
+                    "page-aligned arrays (page-locked at their second call); value and roofline use "
                     "device-resident vectors"}
 
 
@@ -701,8 +713,8 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_host_path:
         try:
-            out["host_path"] = host_path(P, mesh, contacts, r_np, lambda: mas_amd.from_mesh(
-                mesh, max_levels=cfg["levels"], contacts=contacts, device=local))
+            out["host_path"] = host_path(P, mesh, contacts, r_np, lambda **kw: mas_amd.from_mesh(
+                mesh, max_levels=cfg["levels"], contacts=contacts, device=local, **kw))
         except Exception as e:  # context only
             log(f"host path report failed: {e!r}")
 

@@ -54,8 +54,9 @@ extern "C" {
  *    an earlier apply's coarse give-up (MAS_ERR_HIP) before queueing. */
 /* 5: the sharded coarse assembly (mas_prepare_shard_rows / _complete,
  *    mas_set_prepare_allgather; mas_stats.prepare_complete_ms and coarse_split
- *    from the reserved tail, same size); mas_allgather_loopback; the sharded
- *    apply's coarse levels run on the communication stream. */
+ *    from the reserved tail, same size); mas_allgather_loopback;
+ *    mas_config.host_register (from the reserved tail, same size): opt-in
+ *    page-locking of the caller's host arrays. */
 #define MAS_ABI_VERSION 5
 
 typedef enum {
@@ -104,7 +105,16 @@ typedef struct {
                           non-finite pivot: MAS_OK, mas_stats.nonspd_blocks > 0 and a warning in
                           mas_last_error (an SPD but ill-conditioned Hessian can meet one in fp32);
                           1 = such a Prepare fails with MAS_ERR_NOT_SPD */
-    int reserved[8];
+    int host_register; /* ABI 5.  0 = the host-pointer entry points copy through the runtime's
+                          pageable staging (default); 1 = the caller's host arrays are page-locked
+                          (hipHostRegister) when the same (pointer, size) comes back a second time,
+                          so the copies run at the pinned rate.  With 1 the caller promises that a
+                          registered array stays allocated until it passes another array in that
+                          argument or destroys the handle, and that it starts on a page boundary
+                          with its allocation covering its last page whole (posix_memalign /
+                          mmap rounded to pages); an array that does not start on a page is
+                          never registered (its pages may be shared with other allocations) */
+    int reserved[7];
 } mas_config;
 
 typedef struct {

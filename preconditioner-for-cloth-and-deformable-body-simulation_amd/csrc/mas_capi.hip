@@ -209,6 +209,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_EARLY_OD")) h->earlyOd = std::atoi(v);
     if (const char* v = std::getenv("MAS_FOLD_SIDE")) h->foldSide = std::atoi(v);
     if (const char* v = std::getenv("MAS_HIER_CACHE")) h->hierCache = std::atoi(v);
+    h->hostRegister = h->cfg.host_register;
     if (const char* v = std::getenv("MAS_HOST_REGISTER")) h->hostRegister = std::atoi(v);
     if (const char* v = std::getenv("MAS_SHARD_MODE")) h->shardMode = std::atoi(v);
     // MAS_PREP_SERIAL=1 (A/B) queues the early path on the caller's stream: from
@@ -321,13 +322,19 @@ static void pin_host(mas_context* h, int slot, const void* p, size_t bytes) {
         return;
     }
     if (q.registered || q.seen++ != 1) return;  // registered, or found unregistrable
+    // page-aligned arrays only, registered to the end of their last page (the
+    // caller's allocation covers it, mas_config.host_register): registering a
+    // page shared with another allocation would pin, and let the runtime
+    // treat as pinned, memory this handle knows nothing about
+    if (reinterpret_cast<uintptr_t>(p) & 4095) return;
     for (const auto& o : h->pins)  // one registration per array (z and r may be one buffer)
         if (&o != &q && o.registered && o.p == p) return;
     hipPointerAttribute_t attr{};
     const bool pinned = hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost;
     (void)hipGetLastError();
     if (pinned) return;
-    q.registered = hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) == hipSuccess;
+    q.registered = hipHostRegister(const_cast<void*>(p), (bytes + 4095) & ~size_t(4095), hipHostRegisterDefault) ==
+                   hipSuccess;
     (void)hipGetLastError();  // a refused registration leaves the copy pageable, not an error
 }
 

@@ -398,18 +398,21 @@ struct mas_context {
     int rbSeq = 0;
     // staging for host-pointer entry points
     mas::Buffer diagStage, offStage, rangeStage, rStage, zStage;
-    // The caller's host arrays of the host-pointer entry points, page-locked
-    // (hipHostRegister) on first use so their copies run at the pinned rate:
-    // one slot per argument, kept while the same (pointer, size) comes back,
-    // released when another array is passed there and by mas_destroy (env
-    // MAS_HOST_REGISTER=0: never).  Slots: diag, off, ranges, r, z, pcg x, pcg b.
+    // mas_config.host_register = 1 (or env MAS_HOST_REGISTER=1): the caller's
+    // host arrays of the host-pointer entry points, page-locked
+    // (hipHostRegister) when the same (pointer, size) comes back a second
+    // time, page-aligned whole pages only, so their copies run at the pinned
+    // rate: one slot per argument, released when another array is passed
+    // there and by mas_destroy.  Off by default: the library cannot know that
+    // a caller's array outlives its registration.  Slots: diag, off, ranges,
+    // r, z, pcg x, pcg b.
     struct HostPin {
         const void* p = nullptr;
         size_t bytes = 0;
         bool registered = false;
         int seen = 0;  // calls in a row with this (pointer, size); registered at the second
     } pins[7];
-    int hostRegister = 1;
+    int hostRegister = 0;
     // hipcub scratch
     mas::Buffer cubTemp;
     // look-back-free radix sort and scan (rsort.hip): ping-pong keys/values,

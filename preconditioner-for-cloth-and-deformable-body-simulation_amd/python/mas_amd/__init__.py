@@ -54,7 +54,8 @@ class mas_config(ctypes.Structure):
     _fields_ = [("max_levels", ctypes.c_int), ("resort_period", ctypes.c_int), ("fix_vf_bary", ctypes.c_int),
                 ("device", ctypes.c_int), ("keep_blocks", ctypes.c_int),
                 ("reference_formation", ctypes.c_int), ("reference_restriction", ctypes.c_int),
-                ("strict_spd", ctypes.c_int), ("reserved", ctypes.c_int * 8)]
+                ("strict_spd", ctypes.c_int), ("host_register", ctypes.c_int),
+                ("reserved", ctypes.c_int * 7)]
 
 
 class mas_info(ctypes.Structure):
@@ -224,10 +225,11 @@ class SeSchwarzPreconditioner:
 
     def __init__(self, max_levels: int = 0, resort_period: int = 0, fix_vf_bary: bool = False, device: int = -1,
                  keep_blocks: bool = False, reference_formation: bool = False, reference_restriction: bool = False,
-                 strict_spd: bool = False):
+                 strict_spd: bool = False, host_register: bool = False):
         self._L = lib()
         cfg = mas_config(max_levels, resort_period, int(fix_vf_bary), device, int(bool(keep_blocks)),
-                         int(bool(reference_formation)), int(bool(reference_restriction)), int(bool(strict_spd)))
+                         int(bool(reference_formation)), int(bool(reference_restriction)), int(bool(strict_spd)),
+                         int(bool(host_register)))
         h = ctypes.c_void_p()
         rc = self._L.mas_create(ctypes.byref(h), ctypes.byref(cfg))
         if rc != MAS_OK:

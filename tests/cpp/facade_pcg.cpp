@@ -40,20 +40,27 @@ int main(int argc, char** argv) {
     P.m_positions = pos.data();
     P.m_neighbours = &csr;
     P.AllocatePrecoditioner(nV, 0, 0);
+    std::printf("stage allocate\n");
+    std::fflush(stdout);
     std::vector<unsigned> efC(1, 0), eeC(1, 0), vfC(nV + 1, 0);
     P.PreparePreconditioner(diag.data(), off.data(), starts.data(), nullptr, nullptr, nullptr, efC.data(), eeC.data(),
                             vfC.data());
     std::vector<SeVec3fSimd> z(nV);
     P.Preconditioning(z.data(), r0.data(), 3 * nV);
+    std::printf("stage first_apply\n");
+    std::fflush(stdout);
     std::ofstream(d + "/z.bin", std::ios::binary).write(reinterpret_cast<const char*>(z.data()), z.size() * 16);
-    // the host-pointer path again: the caller's arrays are page-locked on
-    // their second use and reused from the library's cache (mas_capi.hip pin_host),
-    // a second Prepare through the same arrays, another output array
+    // the host-pointer path again: a second apply, a second Prepare through
+    // the same arrays, another output array
     {
         std::vector<SeVec3fSimd> z2(nV), z3(nV);
         P.Preconditioning(z2.data(), r0.data(), 3 * nV);
+        std::printf("stage second_apply\n");
+        std::fflush(stdout);
         P.PreparePreconditioner(diag.data(), off.data(), starts.data(), nullptr, nullptr, nullptr, efC.data(),
                                 eeC.data(), vfC.data());
+        std::printf("stage second_prepare\n");
+        std::fflush(stdout);
         P.Preconditioning(z3.data(), r0.data(), 3 * nV);
         const bool same = std::memcmp(z.data(), z2.data(), z.size() * 16) == 0 &&
                           std::memcmp(z.data(), z3.data(), z.size() * 16) == 0;
