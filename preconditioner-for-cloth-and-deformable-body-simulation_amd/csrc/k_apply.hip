@@ -348,12 +348,25 @@ void launch_fine(mas_context* h, int blk0, int blkEnd, const float4* r, float4* 
     const float4* zc = P<float4>(h->Zc);
     const int begin1 = h->levelSize[3], nV = h->nV, var = fine_var(h, blkEnd - blk0);
     const int w = h->rzWpb;
-    switch (L < 4 ? L - 1 : 3) {
-        case 0: launch_fine_n<0>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
-        case 1: launch_fine_n<1>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
-        case 2: launch_fine_n<2>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
-        default: launch_fine_n<3>(var, g, s, inv, blk0, blkEnd, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
+    auto go = [&](int v, int b0, int b1) {
+        const int gg = cdiv(b1 - b0, kApplyThreads / 64);
+        switch (L < 4 ? L - 1 : 3) {
+            case 0: launch_fine_n<0>(v, gg, s, inv, b0, b1, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
+            case 1: launch_fine_n<1>(v, gg, s, inv, b0, b1, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
+            case 2: launch_fine_n<2>(v, gg, s, inv, b0, b1, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
+            default: launch_fine_n<3>(v, gg, s, inv, b0, b1, nV, r, vmap, zc, begin1, z, done, rzPart, w); break;
+        }
+    };
+    // A/B (env MAS_RESIDENT_SPLIT = K): the first K blocks' inverses with
+    // default-policy loads (kept in the Infinity Cache between applies if the
+    // nontemporal stream of the rest does not evict them), the rest
+    // nontemporal, as two launches
+    if (!rzPart && var == 6 && h->residentSplit > 0 && blkEnd - blk0 > h->residentSplit) {
+        go(8, blk0, blk0 + h->residentSplit);
+        go(6, blk0 + h->residentSplit, blkEnd);
+        return;
     }
+    go(var, blk0, blkEnd);
 }
 
 // workgroups of one fine launch of the PCG's applies (= its r.z partials)

@@ -1182,8 +1182,10 @@ int sort_pairs_u32(mas_context* h, const unsigned* kin, unsigned* kout, const in
 int prep_stream_init(mas_context* h) {
     int rc = MAS_OK;
     if (!h->prepStream) {
-        // The fused kernel's queue leaves prepCuReserve CUs (env
-        // MAS_PREP_CU_RESERVE) to the caller's stream: without that the coarse
+        // The fused kernel's queue may leave prepCuReserve CUs (env
+        // MAS_PREP_CU_RESERVE, opt-in since round 6: a CU-masked queue in a
+        // process beside another GPU process stalled its applies, mas_internal.h)
+        // to the caller's stream: without that the coarse
         // assembly gets no slot while the fused kernel's 32 768 waves hold
         // every CU, and the two run one after the other.  The reserved CUs are
         // spread over the mask so that every XCD loses the same number whether
@@ -1203,13 +1205,15 @@ int prep_stream_init(mas_context* h) {
         } else {
             rc = hip_check(h, hipStreamCreateWithFlags(&h->prepStream, hipStreamNonBlocking), "prepare stream");
         }
-        if (rc || (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepFork, hipEventDisableTiming), "event")) ||
-            (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepJoin, hipEventDisableTiming), "event")) ||
-            (rc = hip_check(h, hipEventCreate(&h->evFine[0]), "event")) ||
-            (rc = hip_check(h, hipEventCreate(&h->evFine[1]), "event")) ||
-            (rc = hip_check(h, hipEventCreateWithFlags(&h->evAdd0, hipEventDisableTiming), "event")))
-            return rc;
+        if (rc) return rc;
     }
+    if (!h->evPrepFork &&
+        ((rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepFork, hipEventDisableTiming), "event")) ||
+         (rc = hip_check(h, hipEventCreateWithFlags(&h->evPrepJoin, hipEventDisableTiming), "event")) ||
+         (rc = hip_check(h, hipEventCreate(&h->evFine[0]), "event")) ||
+         (rc = hip_check(h, hipEventCreate(&h->evFine[1]), "event")) ||
+         (rc = hip_check(h, hipEventCreateWithFlags(&h->evAdd0, hipEventDisableTiming), "event"))))
+        return rc;
     return rc;
 }
 

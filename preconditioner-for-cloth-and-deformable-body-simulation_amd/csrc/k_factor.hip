@@ -683,13 +683,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // at 1M + contacts: LDS and VGPRs already allow 8 blocks per CU either way,
 // so it only added a barrier to every step; profiles/round5/ab/.)
 int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hipStream_t s) {
-    // MAS_FACTOR_VARIANT=5: the matrix-core formation (form_mfma, not bitwise)
-    if (blk1 > blk0 && h->factorVariant == 5)
-        k_factor_fused<true><<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
-                                                        P<uint4>(h->valuSlot), blk0, P<int>(h->devStatus));
-    else if (blk1 > blk0)
-        k_factor_fused<false><<<blk1 - blk0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
-                                                         P<uint4>(h->valuSlot), blk0, P<int>(h->devStatus));
+    // The blocks in C launches in a row (round 6): between two of them the
+    // queue waits for the earlier one to drain, and the coarse assembly's
+    // kernels on the caller's queue take the slots it frees -- what the
+    // CU-masked queue did before (mas_internal.h prepCuReserve).  Measured
+    // (steady-state Prepare, device Hessian, ms, profiles/round6/prepare/):
+    // 1M + contacts C = 1 / 2 / 4 / 8 / 12 / 16 -> 2.75 / 2.77 / 2.79 / 2.56 /
+    // 2.70 / 2.75 (32-CU mask 2.45); 4M tet 1 / 4 / 8 / 16 -> 8.88 / 8.33 /
+    // 8.30 / 8.55 (mask 8.58); 256k 1 / 2 / 4 / 8 -> 0.589 / 0.579 / 0.570 /
+    // 0.699; a world-8 rank of 1M 1 / 2 / 4 / 8 -> 1.03 / 1.03 / 0.98 / 1.09.
+    // Env MAS_FUSED_CHUNKS overrides.
+    const int nb = blk1 - blk0;
+    const int chunks = h->fusedChunks > 0 ? h->fusedChunks : nb < 2048 ? 1 : nb <= 16384 ? 4 : 8;
+    for (int c = 0; c < chunks; ++c) {
+        const int b0 = blk0 + (int)((long long)(blk1 - blk0) * c / chunks);
+        const int b1 = blk0 + (int)((long long)(blk1 - blk0) * (c + 1) / chunks);
+        // MAS_FACTOR_VARIANT=5: the matrix-core formation (form_mfma, not bitwise)
+        if (b1 > b0 && h->factorVariant == 5)
+            k_factor_fused<true><<<b1 - b0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
+                                                        P<uint4>(h->valuSlot), b0, P<int>(h->devStatus));
+        else if (b1 > b0)
+            k_factor_fused<false><<<b1 - b0, 64, 0, s>>>(a, P<float>(h->inv), P<uint4>(h->tileSlot),
+                                                         P<uint4>(h->valuSlot), b0, P<int>(h->devStatus));
+    }
     return hip_check(h, hipGetLastError(), "fused factor kernel");
 }
 

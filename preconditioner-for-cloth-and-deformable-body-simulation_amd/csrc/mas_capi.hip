@@ -186,6 +186,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     }
     if (const char* v = std::getenv("MAS_FINE_VARIANT")) h->fineVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_INV_RESIDENT")) h->invResident = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MAS_RESIDENT_SPLIT")) h->residentSplit = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_OCC")) h->coarseOcc = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_NARROW")) h->coarseNarrow = std::atoi(v);
     if (const char* v = std::getenv("MAS_COARSE_WIDE")) h->coarseWide = std::atoi(v);
@@ -204,6 +205,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_C1_CHUNK")) h->c1Chunk = std::atoi(v);
     if (const char* v = std::getenv("MAS_C1_POLL_LIMIT")) h->c1PollLimit = std::atoi(v);
     if (const char* v = std::getenv("MAS_PREP_CU_RESERVE")) h->prepCuReserve = std::atoi(v);
+    if (const char* v = std::getenv("MAS_FUSED_CHUNKS")) h->fusedChunks = std::atoi(v);
     if (const char* v = std::getenv("MAS_FUSED_AFTER_LEVELS")) h->fusedAfterLevels = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_THREAD")) h->earlyThread = std::atoi(v);
     if (const char* v = std::getenv("MAS_EARLY_OD")) h->earlyOd = std::atoi(v);

@@ -217,6 +217,7 @@ struct mas_context {
     // chunking (A/B); 3 = 1 in one-wave workgroups (A/B); 0 = default-policy
     // loads (A/B)
     int fineVariant = 6;
+    int residentSplit = 0;  // env MAS_RESIDENT_SPLIT (A/B, launch_fine): first K blocks default-policy
     int invResident = -1;  // env MAS_INV_RESIDENT: -1 by size (fine_var, k_apply.hip), 0 / 1 forced
     // blocks (waves) per workgroup of the fine kernel in the PCG's applies,
     // one r.z partial per workgroup, summed by every SpMV workgroup (env
@@ -278,9 +279,12 @@ struct mas_context {
     // add0 = level-0 additional rows, evAdd0 = they are ready (k_od waits)
     bool earlyFused = false;
     // CUs the fused kernel's queue leaves to the caller's stream (env
-    // MAS_PREP_CU_RESERVE): 32 since the level maps are reused (1M + contacts,
-    // one box: 0 / 16 / 32 / 48 / 64 -> 3.06 / 3.21 / 2.69 / 2.88 / 2.90 ms)
-    int prepCuReserve = 32;
+    // MAS_PREP_CU_RESERVE; round 4, one box: 0 / 16 / 32 / 48 / 64 -> 3.06 /
+    // 3.21 / 2.69 / 2.88 / 2.90 ms).  0 since round 6: a CU-masked queue kept
+    // alive beside another process's GPU queues left this process's apply
+    // queue unserved (DESIGN.md section 4 "Prepare", round 6)
+    int prepCuReserve = 0;
+    int fusedChunks = 0;  // the fused kernel's launches (launch_factor_fused): 0 = by size, env MAS_FUSED_CHUNKS
     int fusedAfterLevels = 0;  // A/B (env MAS_FUSED_AFTER_LEVELS): the early fused kernel waits for the level build
     int earlyThread = 1;       // the early path queued from a second host thread (env MAS_EARLY_THREAD)
     std::unique_ptr<mas::PrepWorker> prepWorker;  // that thread (created by the first Prepare that needs it)

@@ -16,9 +16,22 @@ contacts = meshgen.vf_contacts(mesh, cfg["contacts"], seed=3) if cfg["contacts"]
 # PREP_SHARD=rank,world: a sharded Prepare (mas_set_prepare_shard) of that rank
 shard = tuple(int(x) for x in os.environ["PREP_SHARD"].split(",")) if os.environ.get("PREP_SHARD") else None
 P = mas_amd.from_mesh(mesh, max_levels=cfg["levels"], contacts=contacts, shard=shard)
+# PREP_DEVICE=1: the Hessian from device memory (mas_prepare_device), so host
+# work inside Prepare is not hidden behind the H2D copies
+dev = None
+if os.environ.get("PREP_DEVICE") == "1":
+    import numpy as np
+    import torch
+    dev = tuple(torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (mesh.diag, mesh.off, mesh.starts))
+    torch.cuda.synchronize()
 for _ in range(reps):
     t0 = time.perf_counter()
-    if contacts is None:
+    if dev is not None:
+        if contacts is None:
+            P.PreparePreconditionerDevice(*dev)
+        else:
+            P.PreparePreconditionerDevice(*dev, None, None, contacts[0], None, None, contacts[1])
+    elif contacts is None:
         P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts)
     else:
         P.PreparePreconditioner(mesh.diag, mesh.off, mesh.starts, None, None, contacts[0], None, None, contacts[1])

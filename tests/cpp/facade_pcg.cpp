@@ -3,6 +3,7 @@
 // simulator that uses the reference would call it.  Inputs come from binary
 // files written by tests/test_gpu_facade.py; z of the first apply and the PCG
 // iteration count are written back for comparison with the oracle.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -100,7 +101,13 @@ int main(int argc, char** argv) {
     double rz = 0;
     for (int i = 0; i < n; ++i) rz += r[i] * zz[i];
     int it = 0;
+    const auto t0 = std::chrono::steady_clock::now();
     for (it = 1; it <= 3000; ++it) {
+        if (it % 25 == 0) {
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            std::printf("stage pcg %d %.1f ms\n", it, ms);
+            std::fflush(stdout);
+        }
         matvec(p, Ap);
         double pAp = 0;
         for (int i = 0; i < n; ++i) pAp += p[i] * Ap[i];

@@ -12,6 +12,55 @@ from conftest import REPO, cloth
 pytestmark = pytest.mark.gpu
 
 
+def _diag(pid):
+    """What a stuck process is doing: each thread's state, wait channel and
+    system call (/proc), and the GPU's activity."""
+    lines = []
+    for t in sorted(os.listdir(f"/proc/{pid}/task")):
+        def rd(name):
+            try:
+                with open(f"/proc/{pid}/task/{t}/{name}") as f:
+                    return f.read().strip()
+            except OSError as e:
+                return f"<{e.__class__.__name__}>"
+        lines.append(f"task {t} {rd('comm')} state={rd('stat').split(') ')[-1][:1]} wchan={rd('wchan')} "
+                     f"syscall={rd('syscall').split(' ')[0]}")
+    for who, q in (("child", pid), ("parent", os.getpid())):
+        try:
+            lines.append(f"kfd queues of the {who}: {len(os.listdir(f'/sys/class/kfd/kfd/proc/{q}/queues'))}")
+        except OSError as e:
+            lines.append(f"kfd queues of the {who}: <{e.__class__.__name__}>")
+    try:
+        smi = subprocess.run(["rocm-smi", "--showuse", "--showmemuse"], capture_output=True, text=True,
+                             timeout=30).stdout
+        lines += [ln for ln in smi.splitlines() if "%" in ln]
+    except Exception as e:  # diagnostics only
+        lines.append(f"rocm-smi: {e!r}")
+    return "\n".join(lines)
+
+
+def _run_watched(cmd, tmp_path, limit=60, env=None):
+    """Run the facade program; if it outlives `limit` s, report how far it got
+    and what it is waiting in, then kill it."""
+    import time
+    log = tmp_path / "facade_stdout.txt"
+    with open(log, "w") as f:
+        p = subprocess.Popen(cmd, stdout=f, stderr=subprocess.STDOUT, env=env)
+        t0 = time.time()
+        while p.poll() is None and time.time() - t0 < limit:
+            time.sleep(0.2)
+        if p.poll() is None:
+            d = _diag(p.pid)
+            time.sleep(2)
+            d2 = _diag(p.pid)
+            p.kill()
+            p.wait()
+            raise AssertionError(f"facade_pcg stuck after {limit} s; output: {log.read_text()!r}\n{d}\n2 s later:\n{d2}")
+    out = log.read_text()
+    assert p.returncode == 0, out
+    return out
+
+
 def test_cpp_facade_pcg(tmp_path):
     import mas_amd
     from mas_amd import meshgen
@@ -26,11 +75,7 @@ def test_cpp_facade_pcg(tmp_path):
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"),
                     os.path.join(REPO, "tests", "cpp", "facade_pcg.cpp"), "-L", lib, "-lSeSchwarzPreconditioner",
                     "-lmas_amd", f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
-    try:
-        out = subprocess.run([str(exe), str(tmp_path)], capture_output=True, text=True, timeout=90,
-                             check=True).stdout
-    except subprocess.TimeoutExpired as e:  # say how far it got
-        raise AssertionError(f"facade_pcg timed out; stdout so far: {e.stdout!r} stderr: {e.stderr!r}")
+    out = _run_watched([str(exe), str(tmp_path)], tmp_path)
     z = np.fromfile(tmp_path / "z.bin", dtype=np.float32).reshape(-1, 4)
     o = Oracle(mesh.nV, 0, 0, 0, 1)
     o.allocate(mesh)
