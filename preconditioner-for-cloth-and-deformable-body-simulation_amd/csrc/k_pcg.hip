@@ -88,6 +88,15 @@ __device__ __forceinline__ float3 mat3_mul(const float* __restrict__ src, float4
                        __fadd_rn(__fadd_rn(__fmul_rn(m[2], x.x), __fmul_rn(m[5], x.y)), __fmul_rn(m[8], x.z)));
 }
 
+// mat3_mul of the transposed block: y_i = sum_j m[3 i + j] x_j, in mat3_mul's
+// order (for a = m^T, mat3_mul(a, x) reads a[i], a[3 + i], a[6 + i] = m[3 i],
+// m[3 i + 1], m[3 i + 2])
+__device__ __forceinline__ float3 mat3_mul_t(const float (&m)[9], float4 x) {
+    return make_float3(__fadd_rn(__fadd_rn(__fmul_rn(m[0], x.x), __fmul_rn(m[1], x.y)), __fmul_rn(m[2], x.z)),
+                       __fadd_rn(__fadd_rn(__fmul_rn(m[3], x.x), __fmul_rn(m[4], x.y)), __fmul_rn(m[5], x.z)),
+                       __fadd_rn(__fadd_rn(__fmul_rn(m[6], x.x), __fmul_rn(m[7], x.y)), __fmul_rn(m[8], x.z)));
+}
+
 __device__ __forceinline__ void add3(float3& a, float3 b) {
     a.x = __fadd_rn(a.x, b.x);
     a.y = __fadd_rn(a.y, b.y);
@@ -154,41 +163,77 @@ constexpr int kSpmvRows = 1;  // row groups per wave and pass
 // load no longer waits for starts.  Entries j >= G (rows longer than G) stay
 // in the CSR arrays.  Same entries on the same lanes in the same order:
 // bitwise equal to the CSR form.
-// MAS_ELL2 (A/B): the neighbour id and the nine components as five float2
-// rows per group (640 floats, the same bytes as 576 + 64): five 8-byte loads
-// per lane and pass instead of ten 4-byte ones
-#ifndef MAS_ELL2
-#define MAS_ELL2 0
-#endif
-constexpr bool kEll2 = MAS_ELL2 != 0;
-template <int G>
+// SYM (A/B, env MAS_PCG_SYM=1; measured slower, so off by default: 1M +
+// contacts SpMV 86 -> 94 us in this layout, 96 and 110 us in two earlier ones,
+// profiles/round6/ab/pcg_sym/ -- the mirrored products cost a cross-lane round
+// trip per pass and the compacted rows' loads wait on a word loaded a pass
+// ahead): the matrix is symmetric block by block
+// wherever the caller's CSR is, so a group's lower entries whose column is
+// in the same group (25 % of the slots of the 1M cloth, 5 % of the 4M tet)
+// need not be stored: the lane of its mirror slot in the same wave row holds
+// the block transposed and forms the slot's product for it (k_pcg_spmv,
+// three floats through ds_bpermute).  Only pairs whose
+// blocks are bitwise transposes of each other are mirrored (checked here,
+// once per solve), so every product -- and the SpMV -- is bitwise the full
+// form's.  The n stored slots of a group are packed at the front of its
+// 576 floats as four rows of component pairs and one row of the last
+// component: (m[2 p], m[2 p + 1]) of the k-th stored slot at float2 p * n + k,
+// m[8] at 8 n + k (n = ellCnt[group]; 48 in the cloth's 2 x 4 patches: each
+// pair row is three whole 128-byte lines, 1 728 bytes per group instead of
+// 2 304, and no line is read by two load instructions -- rows of single
+// components would share lines between neighbouring rows).  ellIdx packs the neighbour id (bits
+// 0-23), whether the slot is mirrored (bit 24) and the stored position k or
+// the mirror slot (bits 25-30); -1 = no entry.
+template <int G, bool SYM>
 __global__ __launch_bounds__(256) void k_pcg_ell(int nV, int nGroups, const int* __restrict__ starts,
                                                  const int* __restrict__ idx, const float* __restrict__ off,
-                                                 float* __restrict__ ellOff, int* __restrict__ ellIdx) {
+                                                 float* __restrict__ ellOff, int* __restrict__ ellIdx,
+                                                 int* __restrict__ ellCnt) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nGroups * 64) return;
     const int gi = t >> 6, slot = t & 63;
-    const int v = gi * (64 / G) + slot / G, j = slot % G;
+    if (gi >= nGroups) return;  // whole waves (nGroups * 64 threads, 256-thread blocks)
+    constexpr int rpg = 64 / G;
+    const int v = gi * rpg + slot / G, j = slot % G;
     int e = -1;
     if (v < nV) {
         const int e0 = starts[v] + j;
         if (e0 < starts[v + 1]) e = e0;
     }
     const int nb = e >= 0 ? idx[e] : -1;
-    if (kEll2) {  // (nb, m0), (m1, m2), ..., (m7, m8) as five float2 rows of 64 slots
-        float2* dst = reinterpret_cast<float2*>(ellOff + (size_t)gi * 640) + slot;
-        float m[9];
+    if (!SYM) {
+        ellIdx[t] = nb;
+        float* dst = ellOff + (size_t)gi * 576 + slot;
 #pragma unroll
-        for (int q = 0; q < 9; ++q) m[q] = e >= 0 ? off[9 * (size_t)e + q] : 0.f;
-        dst[0] = make_float2(__int_as_float(nb), m[0]);
-#pragma unroll
-        for (int k = 1; k < 5; ++k) dst[k * 64] = make_float2(m[2 * k - 1], m[2 * k]);
+        for (int q = 0; q < 9; ++q) dst[q * 64] = e >= 0 ? off[9 * (size_t)e + q] : 0.f;
         return;
     }
-    ellIdx[t] = nb;
-    float* dst = ellOff + (size_t)gi * 576 + slot;
+    int src = -1;  // the mirror slot
+    if (nb >= 0 && nb < v && nb / rpg == gi) {  // a lower entry inside the group: its mirror is in the ELL
+        const int su = starts[nb], eu = min(starts[nb + 1], su + G);
+        for (int k = su; k < eu; ++k) {
+            if (idx[k] != v) continue;
+            bool same = true;
 #pragma unroll
-    for (int q = 0; q < 9; ++q) dst[q * 64] = e >= 0 ? off[9 * (size_t)e + q] : 0.f;
+            for (int q = 0; q < 9; ++q)
+                same = same && __float_as_uint(off[9 * (size_t)e + q]) ==
+                                   __float_as_uint(off[9 * (size_t)k + (q % 3) * 3 + q / 3]);
+            if (same) src = (nb % rpg) * G + (k - su);
+            break;
+        }
+    }
+    const bool stored = nb >= 0 && src < 0;
+    const unsigned long long mask = __ballot(stored);
+    const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+    const int n = __popcll(mask);
+    ellIdx[t] = nb < 0 ? -1 : stored ? (nb | (pos << 25)) : (nb | (1 << 24) | (src << 25));
+    if (stored) {
+        float* g = ellOff + (size_t)gi * 576;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            reinterpret_cast<float2*>(g)[q * n + pos] = make_float2(off[9 * (size_t)e + 2 * q], off[9 * (size_t)e + 2 * q + 1]);
+        g[8 * n + pos] = off[9 * (size_t)e + 8];
+    }
+    if (slot == 0) ellCnt[gi] = n;
 }
 
 // spmv_rows on the ELL form (base is a multiple of 64/G: XcdRows deals whole
@@ -208,18 +253,7 @@ __device__ __forceinline__ void spmv_rows_ell(int base, int nV, int lane, const 
         v[r] = base + r * (64 / G) + lane / G;
         // the matrix streams once per SpMV (302 MB at 1M, beyond the Infinity
         // Cache): nontemporal, so it does not evict the gathered vector
-        if (kEll2) {
-            const float2* src = reinterpret_cast<const float2*>(ellOff + (size_t)(g0 + r) * 640) + lane;
-            const float2 w0 = src[0];
-            nb[r] = __float_as_int(w0.x);
-            m[r][0] = w0.y;
-#pragma unroll
-            for (int k = 1; k < 5; ++k) {
-                const float2 w = src[k * 64];
-                m[r][2 * k - 1] = w.x;
-                m[r][2 * k] = w.y;
-            }
-        } else if (MAS_SPMV_NT) {
+        if (MAS_SPMV_NT) {
             nb[r] = __builtin_nontemporal_load(ellIdx + (size_t)(g0 + r) * 64 + lane);
 #pragma unroll
             for (int q = 0; q < 9; ++q)
@@ -523,25 +557,28 @@ constexpr int kSpmvWaves = MAS_SPMV_WAVES > 0 ? MAS_SPMV_WAVES : 1;
 // One ELL row group's matrix stream: the neighbour ids and the nine
 // component rows of its 64 slots (spmv_rows_ell's layout).
 struct EllSlot {
-    int nb;
+    int nb;  // neighbour id (-1: no entry); SYM: the packed word (k_pcg_ell)
     float m[9];
 };
-template <int G>
+// SYM: w = the group's packed word for this lane and n its stored count,
+// loaded a pass ahead (the component addresses depend on them)
+template <int G, bool SYM>
 __device__ __forceinline__ void ell_load(int g0, int lane, const float* __restrict__ ellOff,
-                                         const int* __restrict__ ellIdx, EllSlot& e) {
-    if (kEll2) {
+                                         const int* __restrict__ ellIdx, int w, int n, EllSlot& e) {
+    if (SYM) {
+        e.nb = w;
+        // a mirrored or empty slot loads the group's first stored block (a line
+        // the stored slots fetch anyway) and ignores it
         typedef float v2 __attribute__((ext_vector_type(2)));
-        const v2* src = reinterpret_cast<const v2*>(ellOff + (size_t)g0 * 640) + lane;
-        const v2 w0 = __builtin_nontemporal_load(src);
-        e.nb = __float_as_int(w0.x);
-        e.m[0] = w0.y;
-        __builtin_amdgcn_sched_barrier(0);  // nb first: the gathers wait for it alone
+        const int k = (w & (1 << 24)) ? 0 : ((w >> 25) & 63);
+        const float* g = ellOff + (size_t)g0 * 576;
 #pragma unroll
-        for (int k = 1; k < 5; ++k) {
-            const v2 w = __builtin_nontemporal_load(src + k * 64);
-            e.m[2 * k - 1] = w.x;
-            e.m[2 * k] = w.y;
+        for (int q = 0; q < 4; ++q) {
+            const v2 t = __builtin_nontemporal_load(reinterpret_cast<const v2*>(g) + q * n + k);
+            e.m[2 * q] = t.x;
+            e.m[2 * q + 1] = t.y;
         }
+        e.m[8] = __builtin_nontemporal_load(g + 8 * n + k);
         return;
     }
     e.nb = __builtin_nontemporal_load(ellIdx + (size_t)g0 * 64 + lane);
@@ -557,12 +594,13 @@ __device__ __forceinline__ void ell_load(int g0, int lane, const float* __restri
 // the unfused form); every row stores its own p into pOut (p_old stays
 // intact for the other rows' gathers).  One launch and one pass over z and p
 // less per iteration; the iterates are bitwise those of the unfused form.
-template <int G, bool FUSE>
-__global__ __launch_bounds__(kPcgThreads) __attribute__((amdgpu_waves_per_eu(kSpmvWaves))) void k_pcg_spmv(int nV, const int* __restrict__ starts,
+template <int G, bool FUSE, bool SYM>
+__global__ __launch_bounds__(kPcgThreads) __attribute__((amdgpu_waves_per_eu(SYM && kSpmvWaves == 1 ? 7 : kSpmvWaves))) void k_pcg_spmv(int nV, const int* __restrict__ starts,
                                                           const int* __restrict__ idx, const float* __restrict__ diag,
                                                           const float* __restrict__ off,
                                                           const float* __restrict__ ellOff,
-                                                          const int* __restrict__ ellIdx, const float4* __restrict__ p,
+                                                          const int* __restrict__ ellIdx, const int* __restrict__ ellCnt,
+                                                          const float4* __restrict__ p,
                                                           float4* __restrict__ ap, PcgState* __restrict__ st,
                                                           double* __restrict__ part, const float4* __restrict__ zf,
                                                           float4* __restrict__ pOut, const double* __restrict__ rzPart,
@@ -588,24 +626,49 @@ __global__ __launch_bounds__(kPcgThreads) __attribute__((amdgpu_waves_per_eu(kSp
         // Branch-free until the products (clamped addresses; a branch would
         // make the compiler drain every load at the join).
         const int lastGroup = (xr.end - 1) / (64 / G);
+        auto groupOf = [&](int base) { return min(base / (64 / G), lastGroup); };
         // one pass: cur's products, nxt's stream issued after cur's gathers;
-        // the two buffers alternate (a register copy would wait for the loads)
-        auto pass = [&](int base, const EllSlot& cur, EllSlot& nxt) {
+        // the two buffers alternate (a register copy would wait for the loads).
+        // SYM: a group's packed words are loaded a pass before its components
+        // (whose addresses they hold), after the current pass's stream, so the
+        // in-order load counter waits for nothing newer; useW is nxt's,
+        // loadW receives the group's after it
+        auto pass = [&](int base, const EllSlot& cur, EllSlot& nxt, int useW, int useN, int& loadW, int& loadN) {
             const int v = base + lane / G;
+            const int curNb = SYM ? (cur.nb < 0 ? -1 : (cur.nb & 0xFFFFFF)) : cur.nb;
             const bool valid = v < nV;
             const int vc = valid ? v : 0;
-            const float4 xn = pv(cur.nb >= 0 ? cur.nb : 0);
+            const float4 xn = pv(curNb >= 0 ? curNb : 0);
             const float4 xd = pv(vc);
             const int e = starts[vc] + sub, e1 = valid ? starts[vc + 1] : 0;
             float dg[9];
             __builtin_memcpy(dg, diag + 9 * (size_t)vc, 36);
-            ell_load<G>(min((base + xr.stride) / (64 / G), lastGroup), lane, ellOff, ellIdx, nxt);
+            ell_load<G, SYM>(groupOf(base + xr.stride), lane, ellOff, ellIdx, useW, useN, nxt);
+            if (SYM) {
+                const int g2 = groupOf(base + 2 * xr.stride);
+                loadW = __builtin_nontemporal_load(ellIdx + (size_t)g2 * 64 + lane);
+                loadN = __builtin_nontemporal_load(ellCnt + g2);
+            }
             const float3 zero = make_float3(0.f, 0.f, 0.f);
             const float3 dp = mat3_mul(dg, xd);
             float3 acc = sub == 0 && valid ? dp : zero;
+            float3 prod = mat3_mul(cur.m, xn);
+            if (SYM) {
+                // A mirrored slot (row v, column u) needs A_vu p_u = B^T p_u, B =
+                // A_uv the block of its mirror slot (row u, column v): that lane
+                // holds B and p_u (its own row's vector) and forms B^T p_u with
+                // the same operations in the same order as mat3_mul on the
+                // transposed block, so the same bits; three floats cross lanes
+                const float3 tp = mat3_mul_t(cur.m, xd);
+                const int a = ((cur.nb >> 25) & 63) << 2;
+                const float3 fromMirror = make_float3(__int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(tp.x))),
+                                                      __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(tp.y))),
+                                                      __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(tp.z))));
+                if (cur.nb >= 0 && ((cur.nb >> 24) & 1)) prod = fromMirror;
+            }
             float3 withN = acc;
-            add3(withN, mat3_mul(cur.m, xn));
-            if (cur.nb >= 0) acc = withN;
+            add3(withN, prod);
+            if (curNb >= 0) acc = withN;
             for (int ee = e + G; ee < e1; ee += G) add3(acc, mat3_mul(off + 9 * (size_t)ee, pv(idx[ee])));
 #pragma unroll
             for (int o = G / 2; o > 0; o >>= 1) {
@@ -620,16 +683,24 @@ __global__ __launch_bounds__(kPcgThreads) __attribute__((amdgpu_waves_per_eu(kSp
             }
         };
         EllSlot a, b;
-        ell_load<G>(min(xr.first / (64 / G), lastGroup), lane, ellOff, ellIdx, a);
+        int wA = 0, wB = 0, nA = 0, nB = 0;
+        if (SYM) {
+            wA = ellIdx[(size_t)groupOf(xr.first) * 64 + lane];
+            nA = ellCnt[groupOf(xr.first)];
+            wB = ellIdx[(size_t)groupOf(xr.first + xr.stride) * 64 + lane];
+            nB = ellCnt[groupOf(xr.first + xr.stride)];
+        }
+        ell_load<G, SYM>(groupOf(xr.first), lane, ellOff, ellIdx, wA, nA, a);
         for (int base = xr.first; base < xr.end;) {
-            pass(base, a, b);
+            pass(base, a, b, wB, nB, wA, nA);
             base += xr.stride;
             if (base >= xr.end) break;
-            pass(base, b, a);
+            pass(base, b, a, wA, nA, wB, nB);
             base += xr.stride;
         }
     } else {
         static_assert(!FUSE || (MAS_SPMV_PIPE && MAS_SPMV_NT && kSpmvRows == 1), "the fused p update needs the pipelined form");
+        static_assert(!SYM || (MAS_SPMV_PIPE && MAS_SPMV_NT && kSpmvRows == 1), "the mirrored layout needs the pipelined form");
         for (int base = xr.first; base < xr.end; base += xr.stride) {
             int v[kSpmvRows];
             float3 y[kSpmvRows];
@@ -744,11 +815,15 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     // the last pass may read up to kSpmvRows - 1 groups past the rows: they
     // are allocated and filled as empty slots (idx -1)
     const int nGroups = cdiv(nV, 64 / G) + kSpmvRows;
-    if ((rc = ensure(h, h->pcgEllOff, (size_t)nGroups * 640 * 4)) ||
-        (rc = ensure(h, h->pcgEllIdx, (size_t)nGroups * 64 * 4)))
+    if ((rc = ensure(h, h->pcgEllOff, (size_t)nGroups * 576 * 4)) ||
+        (rc = ensure(h, h->pcgEllIdx, (size_t)nGroups * 64 * 4)) ||
+        (rc = ensure(h, h->pcgEllCnt, (size_t)nGroups * 4)))
         return rc;
     float* ellOff = P<float>(h->pcgEllOff);
     int* ellIdx = P<int>(h->pcgEllIdx);
+    int* ellCnt = P<int>(h->pcgEllCnt);
+    // the mirrored layout packs neighbour ids into 24 bits
+    const bool sym = h->pcgSym && nV <= (1 << 24);
     // the apply kernels honour the done flag and the fine kernel emits the
     // r.z partials while this solve runs (cleared on every return path)
     const int nRz = precondition ? fine_grid(h) : kPcgBlocks;
@@ -760,7 +835,26 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
     } hooks{h};
     h->applyDone = &st->done;
     h->applyRzPart = rzPart;
-    k_pcg_ell<G><<<cdiv(nGroups * 64, 256), 256, 0, s>>>(nV, nGroups, d_ranges, idx, d_off9, ellOff, ellIdx);
+    if (sym)
+        k_pcg_ell<G, true><<<cdiv(nGroups * 64, 256), 256, 0, s>>>(nV, nGroups, d_ranges, idx, d_off9, ellOff, ellIdx,
+                                                                  ellCnt);
+    else
+        k_pcg_ell<G, false><<<cdiv(nGroups * 64, 256), 256, 0, s>>>(nV, nGroups, d_ranges, idx, d_off9, ellOff,
+                                                                   ellIdx, ellCnt);
+    auto spmv = [&](bool fuse, const float4* pIn, float4* pOut, int itPrev) {
+        if (fuse && sym)
+            k_pcg_spmv<G, true, true><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, ellCnt,
+                                                      pIn, ap, st, part, z, pOut, rzPart, nRz, itPrev);
+        else if (fuse)
+            k_pcg_spmv<G, true, false><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, ellCnt,
+                                                       pIn, ap, st, part, z, pOut, rzPart, nRz, itPrev);
+        else if (sym)
+            k_pcg_spmv<G, false, true><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, ellCnt,
+                                                       pIn, ap, st, part, nullptr, nullptr, nullptr, 0, 0);
+        else
+            k_pcg_spmv<G, false, false><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, ellCnt,
+                                                        pIn, ap, st, part, nullptr, nullptr, nullptr, 0, 0);
+    };
     k_pcg_residual<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, d_x, d_b, r, x64, part);
     k_pcg_start<<<1, b, 0, s>>>(part, st);
     if (precondition) {
@@ -789,11 +883,9 @@ static int pcg_loop(mas_context* h, const float* d_diag9, const float* d_off9, c
             // the fused form: iteration k's p lives in (k even ? p : p2), formed by this SpMV from the last
             float4* pk = fuseP && (k & 1) ? p2 : p;
             if (!fuseP || k == 0)
-                k_pcg_spmv<G, false><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx, pk, ap, st,
-                                                     part, nullptr, nullptr, nullptr, 0, 0);
+                spmv(false, pk, nullptr, 0);
             else
-                k_pcg_spmv<G, true><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, ellOff, ellIdx,
-                                                    (k & 1) ? p : p2, ap, st, part, z, pk, rzPart, nRz, k - 1);
+                spmv(true, (k & 1) ? p : p2, pk, k - 1);
             k_pcg_update_xr<<<g, b, 0, s>>>(nV, k, pk, ap, x64, r, st, part);
             k_pcg_true<G><<<g, b, 0, s>>>(nV, d_ranges, idx, d_diag9, d_off9, x64, d_b, r, st, part);
             if (precondition) {

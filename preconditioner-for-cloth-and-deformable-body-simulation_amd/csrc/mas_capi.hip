@@ -196,6 +196,7 @@ int mas_create(mas_handle* out, const mas_config* cfg) {
     if (const char* v = std::getenv("MAS_REF_RESTRICT")) h->groupedR3 = !std::atoi(v);
     if (const char* v = std::getenv("MAS_FACTOR_VARIANT")) h->factorVariant = std::atoi(v);
     if (const char* v = std::getenv("MAS_PCG_FUSE_P")) h->pcgFuseP = std::atoi(v) != 0;
+    if (const char* v = std::getenv("MAS_PCG_SYM")) h->pcgSym = std::atoi(v) != 0;
     if (const char* v = std::getenv("MAS_RZ_WPB")) {
         const int w = std::atoi(v);
         h->rzWpb = (w == 4 || w == 8) ? w : 2;

@@ -371,8 +371,9 @@ struct mas_context {
     // lowest such block, [2] coarse hand-off waits that gave up (since mas_create)
     mas::Buffer devStatus;
     mas::Buffer pcgVec, pcgPartial, pcgState, pcgStage;  // PCG driver (k_pcg.hip)
-    mas::Buffer pcgEllOff, pcgEllIdx;                    // PCG: the CSR Hessian in wave-slot ELL form
+    mas::Buffer pcgEllOff, pcgEllIdx, pcgEllCnt;         // PCG: the CSR Hessian in wave-slot ELL form
     mas::Buffer pcgRzPart;                               // PCG: r.z partials of the fine apply kernel
+    bool pcgSym = false;   // PCG: A/B (env MAS_PCG_SYM=1): mirrored intra-group blocks not stored (k_pcg_ell; measured slower)
     bool pcgFuseP = true;  // PCG: p = z + beta p inside the next SpMV (env MAS_PCG_FUSE_P=0: its own pass, A/B)
     // set by the PCG driver for the applies of a solve (null otherwise): the
     // apply kernels exit at once when *applyDone != 0, and the fine kernel
@@ -444,7 +445,7 @@ struct mas_context {
                               &tab, &termCnt,
                               &cdCnt, &cdOff, &cdKeys, &cdKeysS, &cdIds, &cdIdsS, &cdVal, &cFineOff, &cdEnt, &c0Ent, &caCnt, &caOff,
                               &caKeys, &caKeysS, &caIds, &caIdsS, &caVal, &cpCnt, &cpOff, &cpKeys, &cpKeysS, &cpIds,
-                              &cpIdsS, &Rc, &Zc, &splitDev, &prepSeg, &prepGathered, &splitPartsDev, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
+                              &cpIdsS, &Rc, &Zc, &splitDev, &prepSeg, &prepGathered, &splitPartsDev, &members, &coarseMask, &shardOff, &shardPos1, &l1src, &deepKeys, &deepVals, &deepIdx, &deepOff, &deepPos, &deepR1, &deepCnt, &deepIdxShard, &c1Tags, &l1info, &pcgVec, &pcgPartial, &pcgState, &pcgStage, &pcgEllOff, &pcgEllIdx, &pcgEllCnt, &pcgRzPart, &shardSeg, &shardGathered, &diagStage, &offStage, &rangeStage, &rStage, &zStage,
                               &cubTemp, &rsKeys, &rsVals, &rsHist, &rsPart, &rsKeysP, &rsValsP, &rsHistP, &rsPartP, &add0, &c0Cnt, &c0Off, &c0Keys, &c0KeysS, &c0Ids, &c0IdsS,
                               &c0Val, &a0Keys, &a0KeysS, &a0Ids, &a0IdsS, &a0Val,
                               &spCst, &spGn, &spVmap, &spCoarseTables, &spFine, &spCoarseMask, &hierFlags, &recRanges,

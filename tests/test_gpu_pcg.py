@@ -178,3 +178,39 @@ def test_inverse_load_policy_bitwise(W, L, monkeypatch):
     assert np.array_equal(z0.view(np.uint32), z1.view(np.uint32))
     assert np.array_equal(x0.view(np.uint32), x1.view(np.uint32))
     assert r0["iterations"] == r1["iterations"] and r0["true_rel_residual"] == r1["true_rel_residual"]
+
+
+@pytest.mark.parametrize("kind,W,L,precondition,fuse,perturb", [
+    ("cloth", 100, 3, True, "1", False), ("cloth", 256, 4, True, "1", False), ("cloth", 101, 3, False, "1", False),
+    ("cloth", 100, 3, True, "0", False), ("tet", 14, 3, True, "1", False), ("cloth", 100, 3, True, "1", True)])
+def test_pcg_mirrored_layout_bitwise(kind, W, L, precondition, fuse, perturb, monkeypatch):
+    """The SpMV's mirrored layout (MAS_PCG_SYM=1, an A/B: a group's lower
+    blocks that are bitwise transposes of an upper block in the same wave row
+    are not stored; the upper block's lane forms their products, k_pcg_ell /
+    k_pcg_spmv) against every block stored (0, the default): the same iterates bit for
+    bit -- x, the iteration counts, the residuals -- on cloth (G = 8, a
+    quarter of the slots mirrored), tet (G = 16), an odd vertex count, the
+    unfused p update, and a Hessian made non-symmetric in every fifth block
+    (those pairs stay stored)."""
+    import mas_amd
+    from mas_amd import meshgen
+    mesh = cloth(W) if kind == "cloth" else tet(W)
+    off = mesh.off
+    if perturb:
+        off = mesh.off.copy()
+        off[::5] *= np.float32(1 + 2 ** -20)
+    b = meshgen.residual(mesh.nV, 23)
+    monkeypatch.setenv("MAS_PCG_FUSE_P", fuse)
+    out = []
+    for sym in ("0", "1"):
+        monkeypatch.setenv("MAS_PCG_SYM", sym)
+        P = mas_amd.from_mesh(mesh, max_levels=L)
+        x, res = P.pcg_solve(mesh.diag, off, mesh.starts, b, max_iters=400 if perturb else 3000, tol=TOL,
+                             precondition=precondition)
+        out.append((x, res))
+    (x0, r0), (x1, r1) = out
+    assert np.array_equal(x0.view(np.uint32), x1.view(np.uint32))
+    for k in ("iterations", "converged", "replacements", "first_pass_iterations", "rel_residual", "true_rel_residual"):
+        assert r0[k] == r1[k], (k, r0[k], r1[k])
+    if not perturb:
+        assert r1["converged"]
