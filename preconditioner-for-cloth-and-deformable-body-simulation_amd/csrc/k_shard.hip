@@ -459,17 +459,11 @@ int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn a
     if (rc) return rc;
     const size_t segBytes = (size_t)sh.seg_max * 16;
     if ((rc = ensure(h, h->shardSeg, segBytes)) || (rc = ensure(h, h->shardGathered, segBytes * world))) return rc;
-    if (!h->commStream) {
-        // the coarse levels run on it beside the level-0 solves: the higher
-        // priority lets their workgroups in ahead of the solves' remaining ones
-        int lo = 0, hi = 0;
-        hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if ((rc = hip_check(h, hipStreamCreateWithPriority(&h->commStream, hipStreamNonBlocking, hi), "comm stream")) ||
-            (rc = hip_check(h, hipEventCreateWithFlags(&h->evRestrict, hipEventDisableTiming), "event")) ||
-            (rc = hip_check(h, hipEventCreateWithFlags(&h->evGathered, hipEventDisableTiming), "event")) ||
-            (rc = hip_check(h, hipEventCreateWithFlags(&h->evShardDone, hipEventDisableTiming), "event")))
-            return rc;
-    }
+    if (!h->evShardDone &&
+        ((rc = hip_check(h, hipEventCreateWithFlags(&h->evRestrict, hipEventDisableTiming), "event")) ||
+         (rc = hip_check(h, hipEventCreateWithFlags(&h->evGathered, hipEventDisableTiming), "event")) ||
+         (rc = hip_check(h, hipEventCreateWithFlags(&h->evShardDone, hipEventDisableTiming), "event"))))
+        return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     // The segments (shardSeg, shardGathered, Rc / Zc) belong to the handle: a
     // call on another stream than the previous one starts after it has ended
@@ -496,6 +490,16 @@ int mas_shard_apply_device(mas_handle h, int rank, int world, mas_allgather_fn a
         if (int e = allgather(seg, gathered, segBytes, s, user))
             return fail(h, MAS_ERR_COMM, "allgather hook returned " + std::to_string(e));
         return mas_apply_shard_finish(h, rank, world, gathered, d_r4, d_z4, s);
+    }
+    if (!h->commStream) {
+        // modes 1 / 2 only (a queue of its own: the default inline form keeps
+        // every kernel on `stream`): the coarse levels run on it beside the
+        // level-0 solves, the higher priority letting their workgroups in
+        // ahead of the solves' remaining ones
+        int lo = 0, hi = 0;
+        hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if ((rc = hip_check(h, hipStreamCreateWithPriority(&h->commStream, hipStreamNonBlocking, hi), "comm stream")))
+            return rc;
     }
     if ((rc = hip_check(h, hipEventRecord(h->evRestrict, s), "record")) ||
         (rc = hip_check(h, hipStreamWaitEvent(h->commStream, h->evRestrict, 0), "comm wait")))
