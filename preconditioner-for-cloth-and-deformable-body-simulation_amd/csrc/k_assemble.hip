@@ -1365,7 +1365,16 @@ static void launch_od(mas_context* h, const FineAsm& fa, hipStream_t s, int v0, 
 }
 
 // od and the record counts in the early path (see run_level0_early)
-bool early_od(const mas_context* h) { return h->earlyOd > 0 || (h->earlyOd < 0 && h->prepWorld > 1); }
+// od and the record counts in the early path: by default for a sharded Prepare
+// and for an unsharded one of 2 048 .. 32 768 level-0 blocks, where the
+// coarse assembly then starts its chain without the od pass (round 6, beside
+// the chunked fused kernel, steady state, ms: 1M + contacts 2.571 -> 2.450,
+// 1M cloth 1.913 -> 1.876, 256k 0.571 -> 0.547; 4M tet 8.27 -> 8.57, so not
+// there; profiles/round6/prepare/r6y, r6z)
+bool early_od(const mas_context* h) {
+    if (h->earlyOd >= 0) return h->earlyOd > 0;
+    return h->prepWorld > 1 || (h->nFineBlk >= 2048 && h->nFineBlk <= 32768);
+}
 
 bool early_fused_wanted(const mas_context* h) {
     const int nv32 = h->nFineBlk * 32;

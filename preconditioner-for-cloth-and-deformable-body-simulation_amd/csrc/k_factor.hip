@@ -692,9 +692,14 @@ int launch_factor_fused(mas_context* h, const FineAsm& a, int blk0, int blk1, hi
     // 2.70 / 2.75 (32-CU mask 2.45); 4M tet 1 / 4 / 8 / 16 -> 8.88 / 8.33 /
     // 8.30 / 8.55 (mask 8.58); 256k 1 / 2 / 4 / 8 -> 0.589 / 0.579 / 0.570 /
     // 0.699; a world-8 rank of 1M 1 / 2 / 4 / 8 -> 1.03 / 1.03 / 0.98 / 1.09.
+    // With od in the early path (early_od: unsharded 2 048 .. 32 768 blocks),
+    // fewer launches do better: 1M + contacts 4 / 6 / 8 -> 2.450 / 2.518 /
+    // 2.569 ms, 256k 2 / 4 -> 0.547 / 0.591 (profiles/round6/prepare/r6y, r6z).
     // Env MAS_FUSED_CHUNKS overrides.
     const int nb = blk1 - blk0;
-    const int chunks = h->fusedChunks > 0 ? h->fusedChunks : nb < 2048 ? 1 : nb <= 16384 ? 4 : 8;
+    int chunks = nb < 2048 ? 1 : nb <= 16384 ? 4 : 8;
+    if (h->prepWorld == 1 && nb >= 2048 && nb <= 32768) chunks = nb <= 8192 ? 2 : 4;
+    if (h->fusedChunks > 0) chunks = h->fusedChunks;
     for (int c = 0; c < chunks; ++c) {
         const int b0 = blk0 + (int)((long long)(blk1 - blk0) * c / chunks);
         const int b1 = blk0 + (int)((long long)(blk1 - blk0) * (c + 1) / chunks);

@@ -294,7 +294,7 @@ struct mas_context {
     bool earlyPlanned = false, earlyPending = false;
     int earlyRc = 0;
     std::string earlyErr;
-    int earlyOd = -1;          // k_od in the early path: 1 always, 0 never, -1 (default) when the Prepare is sharded
+    int earlyOd = -1;          // k_od in the early path: 1 always, 0 never, -1 (default) by early_od's rule
     bool odDone = false;       // this Prepare's od / record counts are queued already
     mas::FineAsm earlyFa{};    // its inputs, kept for launch_level0_fused
     hipEvent_t evAdd0 = nullptr;
